@@ -1,0 +1,156 @@
+/*
+ * nestmc.h -- C-ABI of libnestmc.so, the MI355X (gfx950) engine for the MCMC
+ * inner loop of tkngch/MCMC-for-Nested-Data.
+ *
+ * The reference has no FFI: its hot path is Python (posteriorSampling.py).  Each
+ * entry point below replaces a piece of that Python, cited file:line, and is
+ * bound by the drop-in Python host (mcmc-for-nested-data_amd/nestmc/_lib.py)
+ * through ctypes.  Plain C types only; all host buffers are caller-owned and
+ * copied; device buffers are owned by the context.  Every function returns 0 on
+ * success and a negative code on failure, with the message in nmc_last_error()
+ * (thread-local).  A context is used by one host thread at a time.
+ *
+ * Array layouts (all fp64 unless noted; "c" = local chain, fastest-varying):
+ *   value, log_prior, scale  [P][G][C]       ll           [G][C]
+ *   hyper mu, sigma2         [P][C]          samples      [row][col][C]
+ *   replay z, u              [iter][P][G][C] replay hz, hu [iter][P][C]
+ *   obs                      [n_obs][n_fields] (group-major, CSR by group_offsets)
+ */
+#ifndef NESTMC_H
+#define NESTMC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct nmc_ctx nmc_ctx;
+
+/* pooling: StepMethod subclasses, posteriorSampling.py:662-787 */
+enum { NMC_POOL_COMPLETE = 0, NMC_POOL_NONE = 1, NMC_POOL_PARTIAL = 2 };
+
+/* likelihood families: device restatements of the user logLikelihoodFunction
+ * contract (posteriorSampling.py:61-102) for the models the reference ships or
+ * benchmarks (example/regression.py:53-67, example/distribution.py:18-24, cfg 5).
+ *   NMC_LL_LINREG    obs = [x_1..x_k, y] (+ implicit ones column if consts[1]=1)
+ *                    consts = {k, intercept, sigma (<=0: sigma is the last param)}
+ *   NMC_LL_GAUSS_MEAN obs = [m_0..m_{P-1}]; consts = {sd_0..sd_{P-1}}
+ *   NMC_LL_LOGISTIC  obs = [x_1..x_k, y]; consts = {k, intercept}              */
+enum { NMC_LL_LINREG = 0, NMC_LL_GAUSS_MEAN = 1, NMC_LL_LOGISTIC = 2 };
+
+/* prior families for none/complete pooling: scipy frozen distributions the
+ * reference evaluates with .logpdf (posteriorSampling.py:293-294).
+ * params[8] per parameter = {loc, scale, shape, gammaln(shape), log(scale), 0,0,0}
+ * (gammaln and log(scale) computed on the host with scipy/numpy).            */
+enum { NMC_PRIOR_NORM = 0, NMC_PRIOR_GAMMA = 1, NMC_PRIOR_UNIFORM = 2,
+       NMC_PRIOR_EXPON = 3, NMC_PRIOR_HALFNORM = 4, NMC_PRIOR_CAUCHY = 5,
+       NMC_PRIOR_LAPLACE = 6, NMC_PRIOR_LOGNORM = 7, NMC_PRIOR_INVGAMMA = 8 };
+
+/* random streams: philox = device Philox4x32-10 (replaces numpy legacy MT19937
+ * draws at posteriorSampling.py:306,362,487,498); replay = variates supplied by
+ * nmc_set_replay (captured from the reference, for parity).                    */
+enum { NMC_RNG_PHILOX = 0, NMC_RNG_REPLAY = 1 };
+
+const char* nmc_last_error(void);
+const char* nmc_version(void);
+int nmc_device_count(int* n);
+
+/* Replaces the per-chain StepMethod construction (posteriorSampling.py:517-582,
+ * :1146-1151): CSR offsets (:554-555), data, priors.  chain_base = global id of
+ * local chain 0 (Philox key, posteriorSampling.py:225 seed = chain).           */
+int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base,
+               int n_groups, int n_params, int pooling, int ll_family,
+               const double* ll_consts, int n_ll_consts,
+               const int64_t* group_offsets, const double* obs, int64_t n_obs,
+               int n_fields, const int* prior_family, const double* prior_params,
+               uint32_t seed, int rng_mode);
+int nmc_destroy(nmc_ctx* ctx);
+
+/* Chain state after initialisation (PartialPooling._initialiseParameters /
+ * _determineIndividualStartingPoint :725-758; StepMethod._setStartingPoint
+ * :584-592).  hyper_* may be NULL for none/complete; scale NULL -> 1.0.      */
+int nmc_set_state(nmc_ctx* ctx, const double* value, const double* log_prior,
+                  const double* ll, const double* hyper_mu, const double* hyper_sigma2,
+                  const double* scale);
+int nmc_get_state(nmc_ctx* ctx, double* value, double* log_prior, double* ll,
+                  double* hyper_mu, double* hyper_sigma2, double* scale);
+
+/* Replay variates [n_iter] (RNG mode NMC_RNG_REPLAY). */
+int nmc_set_replay(nmc_ctx* ctx, const double* z, const double* u,
+                   const double* hz, const double* hu, int n_iter);
+
+/* Sampler.sample schedule (posteriorSampling.py:827-860, MCMC.__init__
+ * :1018-1027): allocates the device sample store for every recorded row.     */
+int nmc_set_schedule(nmc_ctx* ctx, int n_iter, int burn, int thin, int tune_interval);
+int nmc_n_rows(nmc_ctx* ctx, int* rows, int* cols);
+
+/* Optional per-step trace [n_iter][P][G][C]: accept flags (uint8) and the
+ * proposal's group log-likelihood; for parity tests.                         */
+int nmc_set_trace(nmc_ctx* ctx, int enable);
+int nmc_get_trace(nmc_ctx* ctx, uint8_t* accept, double* ll_prop);
+
+/* Sampler._loop (posteriorSampling.py:862-896) for iterations [iter_begin,
+ * iter_end): StepMethod.step (:594-613) + HyperParameter.update (:463-498)
+ * + the recorder (:887-889) into the device sample store.  Asynchronous on the
+ * context's stream; call nmc_synchronize before reading results.            */
+int nmc_run(nmc_ctx* ctx, int iter_begin, int iter_end);
+int nmc_synchronize(nmc_ctx* ctx);
+
+/* Recorded rows [row_begin, row_begin+n_rows) as [row][col][C].
+ * Columns follow StepMethod.values / PartialPooling.values (:648-654, :780-787). */
+int nmc_get_samples(nmc_ctx* ctx, int row_begin, int n_rows, double* out);
+/* Total accepted proposals per (p, g, c) since nmc_set_state. */
+int nmc_get_accept_counts(nmc_ctx* ctx, int64_t* out);
+
+/* StepMethod._computeParameterLogLikelihood (:629-635) on device for arbitrary
+ * values theta[P][G][C] -> out[G][C] (used by the host init loop :746-758).  */
+int nmc_eval_group_ll(nmc_ctx* ctx, const double* theta, double* out);
+/* StepMethod.logLikelihood (:656-659): per-observation LL at the current state,
+ * out[C][n_obs] (saveLogLikelihood rows, :907-909).                          */
+int nmc_eval_obs_ll(nmc_ctx* ctx, double* out);
+
+/* Timing on the context's stream (hipEvents). */
+int nmc_event_record(nmc_ctx* ctx, int slot);                 /* slot 0..15 */
+int nmc_event_elapsed(nmc_ctx* ctx, int slot_a, int slot_b, float* ms);
+/* Bracket every step launch with events (adds a little overhead): per-kernel
+ * average duration for the roofline.                                          */
+int nmc_set_kernel_timing(nmc_ctx* ctx, int enable);
+int nmc_get_kernel_timing(nmc_ctx* ctx, double* step_ms_total, int64_t* step_launches,
+                          double* hyper_ms_total, int64_t* hyper_launches);
+int nmc_launch_config(nmc_ctx* ctx, int* waves_per_group, int* chain_blocks);
+
+/* Sampler._printSample (:902-905) + _print (:933-936): append rows of local
+ * chain c to a CSV file with the reference's "%i,%i,%f,..." formatting (and the
+ * header line of :898-900 when header != NULL).  Host only; thread-safe.     */
+int nmc_write_sample_csv(const char* path, int append, const char* header,
+                         const double* samples, int n_chains, int c, int cols,
+                         const int32_t* row_index, int n_rows, int chain_id);
+/* _printLogLikelihood (:907-909): one "%f,..." line per row of ll[n_rows][n]. */
+int nmc_write_ll_csv(const char* path, int append, const double* ll, int64_t n,
+                     int n_rows);
+
+/* Multi-GPU (replaces the process-per-chain fan-out, posteriorSampling.py:182-201):
+ * RCCL communicator over xGMI and ONE gather of every rank's sample store.    */
+int nmc_comm_unique_id(unsigned char* out /* 128 bytes */);
+int nmc_comm_init(void** comm, const unsigned char* id, int nranks, int rank, int device);
+int nmc_comm_destroy(void* comm);
+/* root receives [rank][row][col][C_local] (all ranks must have equal C_local). */
+int nmc_gather_samples(nmc_ctx* ctx, void* comm, int root, double* host_out);
+
+/* Verification hooks (tests only): device numerics on caller inputs.
+ *   prior logpdf of family fam with params[8] at xs[n]   (scipy .logpdf)
+ *   gammainccinv(a[i], q[i]) with lga[i] = gammaln(a[i]) (scipy.special)
+ *   per counter ctr5[i] = (iter, group, param, purpose, chain): out4[i] =
+ *   {Box-Muller normal, uniform a, uniform b, Gamma(gamma_shape) draw}.       */
+int nmc_debug_prior_logpdf(int fam, const double* params8, const double* xs, int n,
+                           double* out);
+int nmc_debug_igamci(const double* a, const double* q, const double* lga, int n,
+                     double* out);
+int nmc_debug_rng(const uint32_t* ctr5, int n, uint32_t seed, double gamma_shape,
+                  double* out4);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NESTMC_H */

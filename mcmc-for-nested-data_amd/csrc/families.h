@@ -1,0 +1,163 @@
+// families.h -- device log-likelihood families (the user logLikelihoodFunction of
+// posteriorSampling.py:61-102, restated per model the reference ships/benchmarks).
+//
+// A family is evaluated chain-on-lane: every lane of a wavefront holds ONE chain's
+// parameter values in registers while the whole wave walks the same observation
+// rows, so row loads are wave-uniform (scalar loads) and each 16-72 byte row feeds
+// 64 chains.  Per family:
+//   Reg      per-lane resolved parameters (built once per group step by prepare())
+//   accum()  per-observation contribution to NACC fp64 accumulators
+//   finish() group log-likelihood from the accumulators and the row count
+//   obs_ll() one observation's log-likelihood in the reference's own formula
+//            (StepMethod.logLikelihood rows, posteriorSampling.py:656-659)
+// Algebra is restructured (e.g. sum r^2 then scale once) but no fast-math: NaN and
+// inf propagate exactly as the reference's MH branches (:347-367) need.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "special.h"
+
+#define NMC_MAXP 16
+
+// ---------------------------------------------------------------------------
+// Gaussian linear regression (example/regression.py:53-67; cfg 3/4 with sigma=1):
+//   rows [x_1..x_K, y] (K = NF-1); params [b0 if intercept, b_1..b_K, sigma if
+//   sigma is sampled].  ll_i = norm(loc=y, scale=sigma).logpdf(yhat),
+//   group LL = -0.5 sum (yhat-y)^2 / sigma^2 - n (log sqrt(2 pi) + log sigma).
+// ---------------------------------------------------------------------------
+template <int NF>
+struct FamLinreg {
+  static constexpr int NFIELDS = NF;
+  static constexpr int NACC = 1;
+  static constexpr int K = NF - 1;
+  int intercept;
+  double sigma_known;   // > 0: fixed noise sd; else sigma is the last parameter
+  double log_sigma_known;
+
+  struct Reg { double b0, b[K > 0 ? K : 1], sig; };
+
+  __device__ __forceinline__ Reg prepare(const double (&th)[NMC_MAXP]) const {
+    Reg r;
+    r.b0 = intercept ? th[0] : 0.0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) r.b[j] = intercept ? th[j + 1] : th[j];
+    r.sig = sigma_known > 0.0 ? sigma_known : (intercept ? th[K + 1] : th[K]);
+    return r;
+  }
+  __device__ __forceinline__ void accum(const Reg& r, const double* __restrict__ row,
+                                        double* acc) const {
+    double yh = r.b0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) yh = fma(row[j], r.b[j], yh);
+    const double e = yh - row[K];
+    acc[0] = fma(e, e, acc[0]);
+  }
+  __device__ __forceinline__ double finish(const Reg& r, const double* acc, long n) const {
+    if (n == 0) return 0.0;
+    const double s = r.sig;
+    if (!(s > 0.0)) return nmc_nan();
+    const double ls = sigma_known > 0.0 ? log_sigma_known : log(s);
+    return -0.5 * (acc[0] / (s * s)) - (double)n * (NMC_LOG_C + ls);
+  }
+  __device__ __forceinline__ double obs_ll(const Reg& r, const double* __restrict__ row) const {
+    double yh = 0.0;
+    if (intercept) yh = r.b0;                        // numpy.sum(X * beta, axis=1)
+#pragma unroll
+    for (int j = 0; j < K; ++j) yh = yh + row[j] * r.b[j];
+    const double s = r.sig;
+    if (!(s > 0.0)) return nmc_nan();
+    const double t = (yh - row[K]) / s;
+    const double ls = sigma_known > 0.0 ? log_sigma_known : log(s);
+    return (-(t * t) / 2.0 - NMC_LOG_C) - ls;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Gaussian means (example/distribution.py:18-24): rows [m_0..m_{P-1}], one field
+// per parameter; ll_i = sum_j norm(m_j, sd_j).logpdf(theta_j).
+// ---------------------------------------------------------------------------
+template <int NF>
+struct FamGaussMean {
+  static constexpr int NFIELDS = NF;
+  static constexpr int NACC = NF;
+  double sd[NF];
+  double lsd[NF];   // log(sd_j), host (numpy) computed
+
+  struct Reg { double t[NF]; };
+
+  __device__ __forceinline__ Reg prepare(const double (&th)[NMC_MAXP]) const {
+    Reg r;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) r.t[j] = th[j];
+    return r;
+  }
+  __device__ __forceinline__ void accum(const Reg& r, const double* __restrict__ row,
+                                        double* acc) const {
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const double e = r.t[j] - row[j];
+      acc[j] = fma(e, e, acc[j]);
+    }
+  }
+  __device__ __forceinline__ double finish(const Reg&, const double* acc, long n) const {
+    if (n == 0) return 0.0;
+    double out = 0.0;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      if (!(sd[j] > 0.0)) return nmc_nan();
+      out += -0.5 * (acc[j] / (sd[j] * sd[j])) - (double)n * (NMC_LOG_C + lsd[j]);
+    }
+    return out;
+  }
+  __device__ __forceinline__ double obs_ll(const Reg& r, const double* __restrict__ row) const {
+    double out = 0.0;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) out = out + nmc_norm_logpdf(r.t[j], row[j], sd[j], lsd[j]);
+    return out;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Logistic regression (cfg 5): rows [x_1..x_K, y]; params [b0 if intercept, b_1..b_K];
+//   eta = b0 + x.b, ll_i = y eta - logaddexp(0, eta).
+// ---------------------------------------------------------------------------
+template <int NF>
+struct FamLogistic {
+  static constexpr int NFIELDS = NF;
+  static constexpr int NACC = 1;
+  static constexpr int K = NF - 1;
+  int intercept;
+
+  struct Reg { double b0, b[K > 0 ? K : 1]; };
+
+  __device__ __forceinline__ Reg prepare(const double (&th)[NMC_MAXP]) const {
+    Reg r;
+    r.b0 = intercept ? th[0] : 0.0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) r.b[j] = intercept ? th[j + 1] : th[j];
+    return r;
+  }
+  __device__ __forceinline__ static double logaddexp0(double eta) {
+    // numpy.logaddexp(0, eta): max + log1p(exp(-|diff|)); NaN propagates
+    if (eta == 0.0) return NMC_LN2;
+    return eta > 0.0 ? eta + log1p(exp(-eta)) : log1p(exp(eta));
+  }
+  __device__ __forceinline__ void accum(const Reg& r, const double* __restrict__ row,
+                                        double* acc) const {
+    double eta = r.b0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) eta = fma(row[j], r.b[j], eta);
+    acc[0] += row[K] * eta - logaddexp0(eta);
+  }
+  __device__ __forceinline__ double finish(const Reg&, const double* acc, long n) const {
+    return n == 0 ? 0.0 : acc[0];
+  }
+  __device__ __forceinline__ double obs_ll(const Reg& r, const double* __restrict__ row) const {
+    double eta = 0.0;
+    if (intercept) eta = r.b0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) eta = eta + row[j] * r.b[j];
+    return row[K] * eta - logaddexp0(eta);
+  }
+};

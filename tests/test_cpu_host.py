@@ -1,0 +1,95 @@
+"""CPU-only checks of the host side: the C-ABI library loads and exports every
+declared symbol (no device calls), family callbacks equal the reference-style
+callbacks bit for bit, priors encode, data generators reproduce the fixtures."""
+
+import os
+import re
+
+import numpy
+import pytest
+import scipy.stats
+
+from golden_cases import Case
+from nestmc import _lib, data, priors
+from nestmc.families import GaussianMean, LinearRegression, Logistic
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "nestmc.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(nmc_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 30
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in _lib.SIGNATURES, "no ctypes signature for %s" % s
+    assert _lib.version().startswith("nestmc")
+
+
+def test_device_count_without_gpu_is_safe():
+    n = _lib.device_count()
+    assert n >= 0
+
+
+def test_families_bit_identical_to_reference_callbacks():
+    from callbacks import ll_distribution, ll_logistic, ll_regression2, ll_regression3
+    r = numpy.random.RandomState(0)
+    c = Case("regression_none")
+    fam = LinearRegression(c.arr["X"], c.arr["y"])
+    par = [r.normal(size=240), r.normal(100, 10, size=240), r.uniform(-0.5, 3, size=240)]
+    assert numpy.array_equal(fam(par), ll_regression3(par, c.arr["X"], c.arr["y"]), equal_nan=True)
+    c = Case("linreg_partial")
+    fam = LinearRegression.simple(c.arr["x"], c.arr["y"], sigma=1.0)
+    par = [r.normal(size=400), r.normal(size=400)]
+    assert numpy.array_equal(fam(par), ll_regression2(par, c.arr["x"], c.arr["y"]))
+    c = Case("logistic_partial")
+    fam = Logistic(c.arr["X"], c.arr["y"])
+    par = [r.normal(size=200) for _ in range(4)]
+    assert numpy.array_equal(fam(par), ll_logistic(par, c.arr["X"], c.arr["y"]))
+    c = Case("distribution_none")
+    sizes = [20] * 4
+    fam = GaussianMean.from_groups(c.arr["mu"], c.arr["sd"], sizes)
+    par = [r.normal(size=80) for _ in range(3)]
+    assert numpy.array_equal(fam(par), ll_distribution(par, c.arr["mu"], c.arr["sd"], sizes))
+
+
+def test_family_layout():
+    x = numpy.arange(6.0)
+    y = 2 * x
+    f = LinearRegression.simple(x, y, sigma=1.0)
+    assert f.n_fields == 2 and f.n_params == 2 and f.intercept
+    assert numpy.array_equal(f.obs(), numpy.stack([x, y], 1))
+    f3 = LinearRegression(numpy.stack([numpy.ones(6), x], 1), y)
+    assert f3.n_params == 3 and f3.consts()[:3] == [1.0, 1.0, 0.0]
+    g = Logistic(numpy.stack([numpy.ones(6), x, x ** 2], 1), (x > 2).astype(float))
+    assert g.n_params == 3 and g.n_fields == 3
+
+
+def test_data_generators_reproduce_fixtures():
+    c = Case("regression_complete")
+    d = data.example_regression(8, 100)
+    assert numpy.array_equal(d["X"], c.arr["X"]) and numpy.array_equal(d["y"], c.arr["y"])
+    c = Case("linreg_partial")
+    x, y, _, _ = data.linreg(8, 50)
+    assert numpy.array_equal(x, c.arr["x"]) and numpy.array_equal(y, c.arr["y"])
+    c = Case("distribution_none")
+    mu, sd = data.example_distribution(3, 4)
+    assert numpy.array_equal(mu, c.arr["mu"]) and numpy.array_equal(sd, c.arr["sd"])
+    c = Case("logistic_partial")
+    X, yl, _ = data.logistic(5, 40, n_coef=4)
+    assert numpy.array_equal(X, c.arr["X"]) and numpy.array_equal(yl, c.arr["y"])
+
+
+def test_prior_encoding():
+    fam, prm = priors.encode(scipy.stats.gamma(10))
+    assert fam == _lib.PRIOR["gamma"] and prm[2] == 10 and prm[1] == 1.0
+    fam, prm = priors.encode(scipy.stats.norm(loc=100, scale=10))
+    assert prm[:2] == [100.0, 10.0] and prm[4] == numpy.log(10.0)
+    with pytest.raises(ValueError):
+        priors.encode(scipy.stats.beta(2, 3))
