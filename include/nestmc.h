@@ -149,6 +149,9 @@ int nmc_debug_igamci(const double* a, const double* q, const double* lga, int n,
                      double* out);
 int nmc_debug_rng(const uint32_t* ctr5, int n, uint32_t seed, double gamma_shape,
                   double* out4);
+/* Diagnostic build only (make stamps -> libnestmc_stamps.so): per-workgroup phase
+ * timestamps of the step kernel, [n_blocks][8] (100 MHz s_memrealtime).       */
+int nmc_debug_stamps(nmc_ctx* ctx, int n_blocks, uint64_t* out);
 
 #ifdef __cplusplus
 }

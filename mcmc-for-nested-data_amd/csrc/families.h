@@ -29,6 +29,7 @@
 template <int NF>
 struct FamLinreg {
   static constexpr int NFIELDS = NF;
+  static constexpr int MAXP = NF + 1;   // parameters a row of NF fields can involve
   static constexpr int NACC = 1;
   static constexpr int K = NF - 1;
   int intercept;
@@ -37,7 +38,7 @@ struct FamLinreg {
 
   struct Reg { double b0, b[K > 0 ? K : 1], sig; };
 
-  __device__ __forceinline__ Reg prepare(const double (&th)[NMC_MAXP]) const {
+  __device__ __forceinline__ Reg prepare(const double* th) const {
     Reg r;
     r.b0 = intercept ? th[0] : 0.0;
 #pragma unroll
@@ -52,6 +53,22 @@ struct FamLinreg {
     for (int j = 0; j < K; ++j) yh = fma(row[j], r.b[j], yh);
     const double e = yh - row[K];
     acc[0] = fma(e, e, acc[0]);
+  }
+  // N rows, written stage by stage so the N dependence chains interleave
+  template <int N>
+  __device__ __forceinline__ void accumN(const Reg& r, const double* __restrict__ rows,
+                                         double (&a)[4][NACC]) const {
+    double yh[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) yh[i] = r.b0;
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+      for (int i = 0; i < N; ++i) yh[i] = fma(rows[i * NF + j], r.b[j], yh[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) yh[i] = yh[i] - rows[i * NF + K];
+#pragma unroll
+    for (int i = 0; i < N; ++i) a[i & 3][0] = fma(yh[i], yh[i], a[i & 3][0]);
   }
   __device__ __forceinline__ double finish(const Reg& r, const double* acc, long n) const {
     if (n == 0) return 0.0;
@@ -80,13 +97,14 @@ struct FamLinreg {
 template <int NF>
 struct FamGaussMean {
   static constexpr int NFIELDS = NF;
+  static constexpr int MAXP = NF + 1;   // parameters a row of NF fields can involve
   static constexpr int NACC = NF;
   double sd[NF];
   double lsd[NF];   // log(sd_j), host (numpy) computed
 
   struct Reg { double t[NF]; };
 
-  __device__ __forceinline__ Reg prepare(const double (&th)[NMC_MAXP]) const {
+  __device__ __forceinline__ Reg prepare(const double* th) const {
     Reg r;
 #pragma unroll
     for (int j = 0; j < NF; ++j) r.t[j] = th[j];
@@ -99,6 +117,17 @@ struct FamGaussMean {
       const double e = r.t[j] - row[j];
       acc[j] = fma(e, e, acc[j]);
     }
+  }
+  template <int N>
+  __device__ __forceinline__ void accumN(const Reg& r, const double* __restrict__ rows,
+                                         double (&a)[4][NACC]) const {
+#pragma unroll
+    for (int j = 0; j < NF; ++j)
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const double e = r.t[j] - rows[i * NF + j];
+        a[i & 3][j] = fma(e, e, a[i & 3][j]);
+      }
   }
   __device__ __forceinline__ double finish(const Reg&, const double* acc, long n) const {
     if (n == 0) return 0.0;
@@ -125,13 +154,14 @@ struct FamGaussMean {
 template <int NF>
 struct FamLogistic {
   static constexpr int NFIELDS = NF;
+  static constexpr int MAXP = NF + 1;   // parameters a row of NF fields can involve
   static constexpr int NACC = 1;
   static constexpr int K = NF - 1;
   int intercept;
 
   struct Reg { double b0, b[K > 0 ? K : 1]; };
 
-  __device__ __forceinline__ Reg prepare(const double (&th)[NMC_MAXP]) const {
+  __device__ __forceinline__ Reg prepare(const double* th) const {
     Reg r;
     r.b0 = intercept ? th[0] : 0.0;
 #pragma unroll
@@ -149,6 +179,19 @@ struct FamLogistic {
 #pragma unroll
     for (int j = 0; j < K; ++j) eta = fma(row[j], r.b[j], eta);
     acc[0] += row[K] * eta - logaddexp0(eta);
+  }
+  template <int N>
+  __device__ __forceinline__ void accumN(const Reg& r, const double* __restrict__ rows,
+                                         double (&a)[4][NACC]) const {
+    double eta[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) eta[i] = r.b0;
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+      for (int i = 0; i < N; ++i) eta[i] = fma(rows[i * NF + j], r.b[j], eta[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) a[i & 3][0] += rows[i * NF + K] * eta[i] - logaddexp0(eta[i]);
   }
   __device__ __forceinline__ double finish(const Reg&, const double* acc, long n) const {
     return n == 0 ? 0.0 : acc[0];

@@ -15,6 +15,7 @@
 #include <string>
 #include <utility>
 #include <vector>
+#include <algorithm>
 
 #include "../../include/nestmc.h"
 #include "kernels.h"
@@ -54,6 +55,9 @@ struct nmc_ctx {
   size_t kev_used = 0, hev_used = 0;
   double step_ms = 0, hyper_ms = 0;
   long long step_n = 0, hyper_n = 0;
+  int stamp_blocks = 0;
+  double* vbuf[2] = {nullptr, nullptr};   // value ping-pong ([P][G][C] each)
+  int vcur = 0;
 };
 
 template <class T>
@@ -125,14 +129,14 @@ static int with_family(nmc_ctx* x, Fn&& fn) {
 static int choose_waves(int CB, int G, int64_t n_obs) {
   if (const char* e = getenv("NMC_WAVES")) {
     int w = atoi(e);
-    if (w >= 1 && w <= 16) return w;
+    if (w >= 1 && w <= 8) return w;
   }
   const int64_t wgs = (int64_t)CB * G;
-  int64_t w = (4096 + wgs - 1) / wgs;                 // ~16 waves per CU on 256 CUs
+  int64_t w = (2048 + wgs - 1) / wgs;                 // ~8 waves per CU on 256 CUs
   const int64_t navg = G > 0 ? n_obs / G : 0;
   const int64_t wmax_rows = navg / 32 > 1 ? navg / 32 : 1;   // >= 32 rows per wave
   if (w > wmax_rows) w = wmax_rows;
-  if (w > 16) w = 16;
+  if (w > 8) w = 8;                 // nmc_k_iter launch bound: 512 threads
   if (w < 1) w = 1;
   return (int)w;
 }
@@ -149,30 +153,46 @@ static int pop_event_pair(nmc_ctx* x, std::vector<std::pair<hipEvent_t, hipEvent
   return 0;
 }
 
+static int nacc_of(const nmc_ctx* x) { return x->family == NMC_LL_GAUSS_MEAN ? x->nf : 1; }
+
+// One launch per iteration: reads the current value buffer, writes the other one.
 template <class Fam>
-static int launch_step(nmc_ctx* x, const Fam& fam, int iter, int p, int hp, int hiter) {
-  const Dev& d = x->d;
-  const int blocks = d.CB * d.G + (hp >= 0 ? d.CB : 0);
-  const size_t lds = d.W > 1 ? (size_t)d.W * 64 * Fam::NACC * sizeof(double) : 0;
+static int launch_iter(nmc_ctx* x, const Fam& fam, int iter) {
+  Dev& d = x->d;
+  const nmc_lds_layout L = nmc_lds(d.stage_rows, Fam::NFIELDS, d.W, Fam::NACC, d.P);
+  const size_t lds = (size_t)L.total * sizeof(double);
+  double* src = x->vbuf[x->vcur];
+  double* dst = x->vbuf[x->vcur ^ 1];
+  d.value = src;
   std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
   if (x->ktiming) {
     if (int rc = pop_event_pair(x, x->kev, x->kev_used, &ev)) return rc;
     HIPCHK(hipEventRecord(ev->first, x->stream));
   }
-  hipLaunchKernelGGL(nmc_k_step<Fam>, dim3(blocks), dim3(64 * d.W), lds, x->stream, d, fam,
-                     d.obs, iter, p, hp, hiter);
+  if (d.stage_rows)
+    hipLaunchKernelGGL((nmc_k_iter<Fam, true>), dim3(d.CB * d.G), dim3(64 * d.W), lds,
+                       x->stream, d, fam, d.obs, (const double*)src, dst, iter);
+  else
+    hipLaunchKernelGGL((nmc_k_iter<Fam, false>), dim3(d.CB * d.G), dim3(64 * d.W), lds,
+                       x->stream, d, fam, d.obs, (const double*)src, dst, iter);
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev->second, x->stream));
+  x->vcur ^= 1;
+  d.value = dst;
   return 0;
 }
 
-static int launch_hyper(nmc_ctx* x, int hp, int hiter) {
+// Gibbs update of every parameter at iteration hiter (closes a chunk of iterations).
+static int launch_hyper(nmc_ctx* x, int hiter) {
   std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
   if (x->ktiming) {
     if (int rc = pop_event_pair(x, x->hev, x->hev_used, &ev)) return rc;
     HIPCHK(hipEventRecord(ev->first, x->stream));
   }
-  hipLaunchKernelGGL(nmc_k_hyper, dim3(x->d.CB), dim3(64), 0, x->stream, x->d, hp, hiter);
+  x->d.value = x->vbuf[x->vcur];
+  const size_t lds = (size_t)12 * x->P * 64 * sizeof(double);
+  hipLaunchKernelGGL(nmc_k_hyper, dim3(x->d.CB), dim3(64 * x->d.W), lds, x->stream, x->d,
+                     hiter);
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev->second, x->stream));
   return 0;
@@ -247,11 +267,12 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   rc |= dalloc(x, &dobs, (size_t)n_obs * n_fields);
   rc |= dalloc(x, &pf, n_params);
   rc |= dalloc(x, &pp, (size_t)8 * n_params);
-  rc |= dalloc(x, &d.value, PGC);
+  rc |= dalloc(x, &x->vbuf[0], PGC);
+  rc |= dalloc(x, &x->vbuf[1], PGC);
+  d.value = x->vbuf[0];
   rc |= dalloc(x, &d.lp, PGC);
   rc |= dalloc(x, &d.ll, GC);
   rc |= dalloc(x, &d.scale, PGC);
-  rc |= dalloc(x, &d.prop, PGC);
   rc |= dalloc(x, &d.nacc, PGC);
   rc |= dalloc(x, &d.nrej, PGC);
   rc |= dalloc(x, &d.tacc, PGC);
@@ -267,6 +288,17 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   d.W = choose_waves(d.CB, n_groups, n_obs);
   d.ha = (n_groups - 1) / 2.0;
   d.hlga = lgamma(d.ha > 0 ? d.ha : 1.0);
+  {
+    // stage each group's rows in LDS when the whole workgroup carve fits 96 KiB
+    int64_t nmax = 0;
+    for (int g = 0; g < n_groups; ++g)
+      nmax = std::max<int64_t>(nmax, group_offsets[g + 1] - group_offsets[g]);
+    const int nacc = ll_family == NMC_LL_GAUSS_MEAN ? n_fields : 1;
+    const nmc_lds_layout L = nmc_lds((int)std::min<int64_t>(nmax, 1 << 20), n_fields, d.W,
+                                     nacc, n_params);
+    d.stage_rows = ((size_t)L.total * 8 <= (size_t)96 * 1024 && !getenv("NMC_NO_STAGE"))
+                       ? (int)nmax : 0;
+  }
   d.thin = 1; d.tune_interval = 100;
   HIPCHK(hipMemcpy(off, group_offsets, (n_groups + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
   if (n_obs > 0)
@@ -382,6 +414,20 @@ int nmc_set_schedule(nmc_ctx* x, int n_iter, int burn, int thin, int tune_interv
   dfree(x, d.samples);
   int rc = dalloc(x, &d.samples, (size_t)rows * d.cols * x->C);
   if (rc) return rc;
+  // variate ring: a chunk of iterations' worth of pre-drawn variates (<= ~1 GiB)
+  const size_t per_iter = ((size_t)2 * x->P * x->G * x->C + (size_t)2 * x->P * x->C) * 8;
+  size_t budget = (size_t)1 << 30;
+  if (const char* e = getenv("NMC_VARIATE_BYTES")) budget = (size_t)atoll(e);
+  int vcap = (int)(budget / per_iter);
+  if (vcap < 1) vcap = 1;
+  if (vcap > n_iter) vcap = n_iter > 0 ? n_iter : 1;
+  dfree(x, d.vz); dfree(x, d.vlu); dfree(x, d.vhz); dfree(x, d.vhx);
+  const size_t PGC = (size_t)x->P * x->G * x->C, PC = (size_t)x->P * x->C;
+  rc = dalloc(x, &d.vz, vcap * PGC) | dalloc(x, &d.vlu, vcap * PGC) |
+       dalloc(x, &d.vhz, vcap * PC) | dalloc(x, &d.vhx, vcap * PC);
+  if (rc) return rc;
+  d.vcap = vcap;
+  d.vbase = 0;
   x->n_iter = n_iter;
   x->scheduled = true;
   return alloc_trace(x);
@@ -418,27 +464,21 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
     return fail(-1, "replay variates do not cover the iteration range");
   const bool partial = x->pooling == NMC_POOL_PARTIAL;
   const int P = x->P;
-  {
-    const size_t n = (size_t)P * x->G * x->C;
-    const int blocks = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
-    hipLaunchKernelGGL(nmc_k_prop, dim3(blocks), dim3(256), 0, x->stream, x->d, iter_begin);
-    HIPCHK(hipGetLastError());
-  }
   return with_family(x, [&](auto fam) -> int {
-    for (int it = iter_begin; it < iter_end; ++it) {
-      for (int p = 0; p < P; ++p) {
-        int hp = -1, hiter = -1;
-        if (partial && P >= 2) {
-          if (p > 0) { hp = p - 1; hiter = it; }
-          else if (it > iter_begin) { hp = P - 1; hiter = it - 1; }
-        }
-        if (int rc = launch_step(x, fam, it, p, hp, hiter)) return rc;
-        if (partial && P == 1)
-          if (int rc = launch_hyper(x, 0, it)) return rc;
-      }
+    for (int c0 = iter_begin; c0 < iter_end; c0 += x->d.vcap) {
+      const int c1 = c0 + x->d.vcap < iter_end ? c0 + x->d.vcap : iter_end;
+      // every variate of iterations [c0, c1) in one fully parallel launch
+      x->d.vbase = c0;
+      const size_t n = (size_t)(c1 - c0) * P * x->C * (x->G + (partial ? 1 : 0));
+      const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);
+      hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);
+      HIPCHK(hipGetLastError());
+      for (int it = c0; it < c1; ++it)
+        if (int rc = launch_iter(x, fam, it)) return rc;
+      // close the chunk: the last Gibbs update reads this chunk's variates
+      if (partial)
+        if (int rc = launch_hyper(x, c1 - 1)) return rc;
     }
-    if (partial && P >= 2)
-      if (int rc = launch_hyper(x, P - 1, iter_end - 1)) return rc;
     return 0;
   });
 }
@@ -478,7 +518,7 @@ int nmc_eval_group_ll(nmc_ctx* x, const double* theta, double* out) {
   HIPCHK(hipMemcpyAsync(th, theta, PGC * 8, hipMemcpyHostToDevice, x->stream));
   int rc = with_family(x, [&](auto fam) -> int {
     using F = decltype(fam);
-    const size_t lds = x->d.W > 1 ? (size_t)x->d.W * 64 * F::NACC * sizeof(double) : 0;
+    const size_t lds = (size_t)x->d.W * 64 * F::NACC * sizeof(double);
     hipLaunchKernelGGL(nmc_k_group_ll<F>, dim3(x->d.CB * x->G), dim3(64 * x->d.W), lds,
                        x->stream, x->d, fam, x->d.obs, (const double*)th, o);
     HIPCHK(hipGetLastError());
@@ -691,6 +731,27 @@ int nmc_debug_prior_logpdf(int fam, const double* prm8, const double* xs, int n,
   HIPCHK(hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost));
   hipFree(dp); hipFree(dx); hipFree(dout);
   return 0;
+}
+
+int nmc_debug_stamps(nmc_ctx* x, int n_blocks, uint64_t* out) {
+  // n_blocks > 0: (re)allocate and zero [n_blocks][8]; out != NULL: copy back.
+  hipSetDevice(x->device);
+  if (n_blocks > 0) {
+    dfree(x, x->d.stamps);
+    x->d.stamps = nullptr;
+    if (int rc = dalloc(x, &x->d.stamps, (size_t)n_blocks * 8)) return rc;
+    HIPCHK(hipMemset(x->d.stamps, 0, (size_t)n_blocks * 64));
+    x->stamp_blocks = n_blocks;
+  }
+  if (out) {
+    HIPCHK(hipStreamSynchronize(x->stream));
+    HIPCHK(hipMemcpy(out, x->d.stamps, (size_t)x->stamp_blocks * 64, hipMemcpyDeviceToHost));
+  }
+#ifdef NMC_STAMPS
+  return 0;
+#else
+  return fail(-1, "not a stamps build (make stamps)");
+#endif
 }
 
 int nmc_debug_igamci(const double* a, const double* q, const double* lga, int n, double* out) {

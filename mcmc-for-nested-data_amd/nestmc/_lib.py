@@ -79,6 +79,7 @@ SIGNATURES = {
                                         _c_double_p]),
     "nmc_debug_rng": (ctypes.c_int, [_c_uint32_p, ctypes.c_int, ctypes.c_uint32,
                                      ctypes.c_double, _c_double_p]),
+    "nmc_debug_stamps": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
 }
 
 _lib = None

@@ -1,0 +1,216 @@
+"""samplePosterior on the GPU: the reference's API and files, the device's loop.
+
+Control flow of posteriorSampling.samplePosterior (:28-216) with the per-chain
+Python hot loop (MCMC/Sampler/StepMethod, :790-1158) replaced by libnestmc:
+
+  validate + prepare directories/logs        (:147-168, :1018-1043)
+  host init of every chain, RandomState(c)   (:1060-1141, :725-758)   nestmc.init
+  shard chains over GPUs (contiguous blocks of global chain ids)      nestmc.parallel
+  device loop: nmc_run over all iterations   (:862-896)               nestmc.engine
+  device sample store -> sample.<c>.csv      (:898-936)               nestmc.output
+  optional per-observation LL rows           (:890-891, :907-909)
+
+The product path never falls back to the CPU: a likelihood that is not a device
+family (nestmc.families) or a missing GPU/library raises.
+"""
+
+import datetime
+import os
+
+import numpy
+
+from . import _lib
+from . import output
+from .engine import Engine
+from .families import is_family
+from .init import init_chains
+from .parallel import shard
+
+
+def schedule(n_iter, n_samples):
+    """MCMC.__init__ burn/thin (posteriorSampling.py:1018-1027)."""
+    if n_iter < n_samples:
+        print("nIter (%i) cannot be less than nSamples (%i)." % (n_iter, n_samples))
+        raise Exception()
+    burn = n_iter // 2 if n_iter // 2 > n_samples else n_iter - n_samples
+    thin = int(numpy.ceil((n_iter - burn) / n_samples))
+    return burn, thin
+
+
+def record_iterations(n_iter, burn, thin):
+    return [i for i in range(n_iter) if i % thin == 0 and i >= burn]
+
+
+def _sizes(n_groups, n_responses, pooling):
+    if isinstance(n_responses, (int, numpy.integer)):
+        sizes = [int(n_responses)] * n_groups
+    else:
+        sizes = [int(v) for v in n_responses]       # list or tuple (the reference: list only)
+        if len(sizes) != n_groups:
+            raise ValueError("nResponsesPerGroup needs one entry per group")
+    if pooling == "complete":
+        sizes = [int(sum(sizes))]                  # CompletePooling: one group (:667-671)
+    return sizes
+
+
+def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponsesPerGroup,
+                     pooling, logLikelihoodFunction, outputDirectory, saveLogLikelihood=True,
+                     priorDistribution=None, startWithMLE=False, startingPointValueRange=None,
+                     nProcesses=1, displayProgress=True, loggingLevel="info", *,
+                     seed=0, devices=None, rng="philox", chains=None, return_samples=False,
+                     write_files=True):
+    """Drop-in for posteriorSampling.samplePosterior (same positional/keyword API).
+
+    Extra keyword-only options (all optional):
+      seed       Philox seed (key = (global chain id, seed)); default 0
+      devices    GPU ids to shard chains over (default: [0]); chains are split in
+                 contiguous blocks so chain c always draws the same stream
+      rng        "philox" (default) or "replay" (test use)
+      chains     run only these global chain ids (multi-process sharding)
+      return_samples  also return {"rows": [C][rows][cols], "row_index", "header"}
+    nProcesses sizes the host threads used for chain initialisation and CSV writing.
+    """
+    start_time = datetime.datetime.now()
+    if not is_family(logLikelihoodFunction):
+        raise TypeError(
+            "logLikelihoodFunction must be a nestmc device family (nestmc.LinearRegression, "
+            "GaussianMean, Logistic): an arbitrary Python callable cannot run on the GPU")
+    if pooling not in ("partial", "none", "complete"):
+        raise Exception("Invalid pooling: ", pooling)
+    names = tuple(parameterName)
+    if len(names) != logLikelihoodFunction.n_params:
+        raise ValueError("parameterName has %d names, the likelihood family has %d parameters"
+                         % (len(names), logLikelihoodFunction.n_params))
+    if nProcesses is None or nProcesses <= 0:
+        nProcesses = os.cpu_count() or 1
+    threads = max(1, min(int(nProcesses), 64))
+
+    if write_files:
+        sample_dir, log_dir = output.prepare_directories(outputDirectory)
+        logger = output.get_logger(log_dir + "samplePosterior.log", "samplePosterior",
+                                   loggingLevel)
+    else:
+        sample_dir = log_dir = None
+        logger = None
+    msg = "MCMC sampling.\n\tpooling: %s.\n\tnChains: %i, nIterPerChain: %i, " \
+          "nSamplesPerChain: %i." % (pooling, nChains, nIter, nSamples)
+    if logger:
+        logger.info(msg)
+    if displayProgress:
+        print(msg)
+
+    burn, thin = schedule(nIter, nSamples)
+    sizes = _sizes(nGroups, nResponsesPerGroup, pooling)
+    G = len(sizes)
+    priors = None
+    if pooling in ("none", "complete"):
+        if priorDistribution is None or len(priorDistribution) != len(names):
+            raise ValueError("Invalid prior")
+        priors = list(priorDistribution)
+    elif priorDistribution is not None and logger:
+        logger.info("Partial pooling ignores prior distribution.")
+    if pooling == "partial" and G < 2:
+        raise ValueError("partial pooling needs at least two groups (the invgamma update of "
+                         "posteriorSampling.py:494-498 has shape (G-1)/2)")
+
+    chain_ids = list(range(nChains)) if chains is None else [int(c) for c in chains]
+    if _lib.device_count() < 1:
+        raise _lib.NestmcError("no HIP device visible: the sampler runs on MI355X only")
+    devices = [0] if devices is None else list(devices)
+    partial = pooling == "partial"
+
+    # ---- host initialisation (reference RNG order, RandomState(chain)) -----
+    if displayProgress:
+        output.print_progress("Initialising %d chains." % len(chain_ids))
+    chain_logs = []
+    if logger:
+        for c in chain_ids:
+            lg = output.get_logger(log_dir + "/mcmc.chain%.2i.log" % c, "mcmc.chain%.2i" % c,
+                                   loggingLevel)
+            lg.info("chain %i. Started looking for a reasonable starting state." % c)
+            chain_logs.append(lg)
+    st = init_chains(logLikelihoodFunction, sizes, names, chain_ids, pooling, priors,
+                     startingPointValueRange, startWithMLE, threads=threads)
+
+    # ---- shard contiguous blocks of chains over the devices -----------------
+    engines = []
+    for r, dev in enumerate(devices):
+        s0, cnt = shard(len(chain_ids), len(devices), r)
+        if cnt == 0:
+            continue
+        ids = chain_ids[s0:s0 + cnt]
+        if ids != list(range(ids[0], ids[0] + cnt)):
+            raise ValueError("chains must be contiguous global ids per device")
+        eng = Engine(logLikelihoodFunction, sizes, cnt, pooling, priors, seed=seed,
+                     chain_base=ids[0], device=dev, rng=rng)
+        sl = slice(s0, s0 + cnt)
+        eng.set_state(st["value"][sl], st["log_prior"][sl], st["ll"][sl],
+                      None if st["mu"] is None else st["mu"][sl],
+                      None if st["s2"] is None else st["s2"][sl])
+        eng.set_schedule(nIter, burn, thin, 100)
+        engines.append((eng, s0, ids))
+
+    # ---- the device loop ----------------------------------------------------
+    rec = record_iterations(nIter, burn, thin)
+    if displayProgress:
+        output.print_progress("Sampling started. 0% complete.")
+    t_loop = datetime.datetime.now()
+    if saveLogLikelihood and write_files:
+        # per recorded row: advance to it, evaluate every observation's LL (:656-659)
+        prev = 0
+        for i in rec:
+            for eng, _, _ in engines:
+                eng.run(prev, i + 1)
+            for eng, _, ids in engines:
+                ll = eng.eval_obs_ll()
+                output.append_ll_rows(sample_dir, ll[:, None, :], ids)
+            prev = i + 1
+        for eng, _, _ in engines:
+            eng.run(prev, nIter)
+    else:
+        steps = 10 if displayProgress and nIter >= 10 else 1
+        bounds = [round(nIter * k / steps) for k in range(steps + 1)]
+        for k in range(steps):
+            for eng, _, _ in engines:
+                eng.run(bounds[k], bounds[k + 1])
+            if displayProgress and steps > 1:
+                for eng, _, _ in engines:
+                    eng.synchronize()
+                output.print_progress("%i%% complete." % (100 * (k + 1) // steps))
+    for eng, _, _ in engines:
+        eng.synchronize()
+    loop_seconds = (datetime.datetime.now() - t_loop).total_seconds()
+
+    # ---- samples -> files ----------------------------------------------------
+    header = output.header_names(names, G, partial)
+    rows_all = []
+    for eng, s0, ids in engines:
+        raw = eng.samples_raw()                     # [rows][cols][C_local]
+        if write_files:
+            hdr = header if burn < nIter else None
+            output.write_sample_csvs(sample_dir, raw, list(range(len(ids))), ids, hdr, rec,
+                                     threads=threads)
+        if return_samples:
+            rows_all.append(numpy.transpose(raw, (2, 0, 1)))
+    accept = [eng.accept_counts() for eng, _, _ in engines] if return_samples else None
+    for eng, _, _ in engines:
+        eng.close()
+
+    elapsed = datetime.datetime.now() - start_time
+    msg = "Finished. The elapsed time in total is %s." \
+        % datetime.timedelta(seconds=int(elapsed.total_seconds()))
+    if logger:
+        for lg in chain_logs:
+            lg.info("100% complete.")
+            output.close_logger(lg)
+        logger.info(msg)
+        output.close_logger(logger)
+    if displayProgress:
+        print("")
+        output.print_progress(msg)
+    if return_samples:
+        return {"rows": numpy.concatenate(rows_all, axis=0), "row_index": rec,
+                "header": header, "burn": burn, "thin": thin,
+                "accepted": numpy.concatenate(accept, axis=0),
+                "loop_seconds": loop_seconds}
+    return None

@@ -1,0 +1,99 @@
+#!/usr/bin/env python
+"""Kernel-level sweep (diagnostics, not the contract bench): per-launch step-kernel
+time for the cfg-3 workload under different poolings / waves-per-group, so the
+Metropolis step, the Gibbs update and launch overhead can be told apart."""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mcmc-for-nested-data_amd"))
+
+import numpy  # noqa: E402
+import scipy.stats  # noqa: E402
+
+from nestmc import data  # noqa: E402
+from nestmc.engine import Engine  # noqa: E402
+from nestmc.families import LinearRegression, Logistic, GaussianMean  # noqa: E402
+
+
+def engine_for(kind, C, G, N, pooling, waves):
+    if waves:
+        os.environ["NMC_WAVES"] = str(waves)
+    else:
+        os.environ.pop("NMC_WAVES", None)
+    r = numpy.random.RandomState(0)
+    if kind == "linreg":
+        x, y, _, _ = data.linreg(G, N, seed=7)
+        fam = LinearRegression.simple(x, y, sigma=1.0)
+        start = numpy.array([0.0, 2.0])
+    elif kind == "logistic":
+        X, y, _ = data.logistic(G, N, n_coef=8, seed=1)
+        fam = Logistic(X, y)
+        start = numpy.zeros(8)
+    else:
+        mu, sd = data.example_distribution(3, G)
+        fam = GaussianMean.from_groups(mu, sd, [N] * G)
+        start = numpy.zeros(3)
+    P = fam.n_params
+    priors = [scipy.stats.norm(0, 10)] * P if pooling != "partial" else None
+    eng = Engine(fam, [N] * G, C, pooling, priors, seed=1)
+    value = start[None, :, None] + 0.1 * r.normal(size=(C, P, G))
+    if pooling == "partial":
+        mu = numpy.tile(start, (C, 1))
+        s2 = numpy.full((C, P), 0.5)
+        lp = numpy.zeros((C, P, G))
+        ll = eng.eval_group_ll(value)
+        eng.set_state(value, lp, ll, mu, s2)
+    else:
+        lp = numpy.zeros((C, P, G))
+        eng.set_state(value, lp, numpy.full((C, G), numpy.nan))
+    return eng, fam
+
+
+def run(kind, C, G, N, pooling, waves, iters):
+    eng, fam = engine_for(kind, C, G, N, pooling, waves)
+    eng.set_schedule(3 * iters, 3 * iters, 1)
+    eng.run(0, iters)
+    eng.synchronize()
+    eng.event_record(0)
+    t0 = time.perf_counter()
+    eng.run(iters, 2 * iters)
+    eng.event_record(1)
+    eng.synchronize()
+    wall = time.perf_counter() - t0
+    ms = eng.event_elapsed_ms(0, 1)
+    eng.set_kernel_timing(True)
+    eng.run(2 * iters, 3 * iters)
+    kt = eng.kernel_timing()
+    cfg = eng.launch_config()
+    eng.close()
+    rate = C * G * iters / (ms / 1e3)
+    return dict(kind=kind, C=C, G=G, N=N, pooling=pooling, waves=cfg["waves_per_group"],
+                us_per_iter=ms * 1e3 / iters, wall_us_per_iter=wall * 1e6 / iters,
+                step_us=kt["step_ms"] * 1e3 / max(1, kt["step_launches"]),
+                hyper_us=kt["hyper_ms"] * 1e3 / max(1, kt["hyper_launches"]),
+                rate=rate)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=300)
+    ap.add_argument("--quick", action="store_true")
+    a = ap.parse_args()
+    cases = [("linreg", 256, 64, 1000, "partial", w) for w in (0, 2, 4, 8)]
+    cases += [("linreg", 256, 64, 1000, "none", w) for w in (0, 4, 8)]
+    if not a.quick:
+        cases += [("linreg", 1024, 256, 2000, "partial", 0),
+                  ("gauss", 256, 32, 500, "none", 0),
+                  ("logistic", 64, 128, 5000, "partial", 0)]
+    for c in cases:
+        iters = a.iters if c[3] * c[1] * c[2] < 5e7 else max(20, a.iters // 10)
+        print(json.dumps(run(*c, iters)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
