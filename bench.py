@@ -177,9 +177,11 @@ def main():
     launches = kt["step_launches"]
     avg_step_ms = kt["step_ms"] / max(1, launches)
     b_obs = fam.bytes_per_obs()
-    bytes_per_launch = C * G * N * b_obs          # one parameter step streams each group once
+    # one launch = one iteration = P parameter steps; SURVEY 8(d): B_unit = P*N*b_obs
+    # per chain*group*iteration (each step streams the group's rows once per chain)
+    bytes_per_launch = C * G * P * N * b_obs
     achieved_gbs = bytes_per_launch / (avg_step_ms * 1e-3) / 1e9
-    flops_per_launch = C * G * N * 5              # fma + sub + fma per (chain, obs)
+    flops_per_launch = C * G * P * N * 5          # fma + sub + fma per (chain, obs, step)
     fp64_tflops = flops_per_launch / (avg_step_ms * 1e-3) / 1e12
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "hbm_traffic_r01.json")
@@ -217,7 +219,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "kernel": "nmc_k_step<FamLinreg<2>>",
+                         "kernel": "nmc_k_iter<FamLinreg<2>, true>",
                          "avg_launch_us": avg_step_ms * 1e3,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "fp64_valu": {"achieved": fp64_tflops, "peak": FP64_VALU_PEAK_TFLOPS,

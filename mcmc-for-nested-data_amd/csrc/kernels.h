@@ -300,11 +300,7 @@ __device__ __forceinline__ void nmc_ll_chunk(const Fam& fam, const typename Fam:
       double nxt[R * NF];
 #pragma unroll
       for (int j = 0; j < R * NF; ++j) nxt[j] = q[j];
-      // keep the next block's reads issued BEFORE this block's math (the scheduler
-      // would otherwise sink them below it and expose the full read latency)
-      __builtin_amdgcn_sched_barrier(0);
       fam.template accumN<R>(reg, cur, a);
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < R * NF; ++j) cur[j] = nxt[j];
     }
