@@ -12,6 +12,7 @@
  *
  * Array layouts (all fp64 unless noted; "c" = local chain, fastest-varying):
  *   value, log_prior, scale  [P][G][C]       ll           [G][C]
+ *   (on the device the values after iteration t live in one of two buffers, t & 1)
  *   hyper mu, sigma2         [P][C]          samples      [row][col][C]
  *   replay z, u              [iter][P][G][C] replay hz, hu [iter][P][C]
  *   obs                      [n_obs][n_fields] (group-major, CSR by group_offsets)
@@ -114,11 +115,13 @@ int nmc_eval_obs_ll(nmc_ctx* ctx, double* out);
 int nmc_event_record(nmc_ctx* ctx, int slot);                 /* slot 0..15 */
 int nmc_event_elapsed(nmc_ctx* ctx, int slot_a, int slot_b, float* ms);
 /* Bracket every step launch with events (adds a little overhead): per-kernel
- * average duration for the roofline.                                          */
+ * average duration for the roofline; step_iters = iterations those launches ran. */
 int nmc_set_kernel_timing(nmc_ctx* ctx, int enable);
 int nmc_get_kernel_timing(nmc_ctx* ctx, double* step_ms_total, int64_t* step_launches,
-                          double* hyper_ms_total, int64_t* hyper_launches);
-int nmc_launch_config(nmc_ctx* ctx, int* waves_per_group, int* chain_blocks);
+                          int64_t* step_iters, double* hyper_ms_total, int64_t* hyper_launches);
+/* Launch geometry: waves per workgroup, 64-chain blocks, and whether one resident
+ * launch runs a whole chunk of iterations (1) or one launch per iteration (0).   */
+int nmc_launch_config(nmc_ctx* ctx, int* waves_per_group, int* chain_blocks, int* persistent);
 
 /* Sampler._printSample (:902-905) + _print (:933-936): append rows of local
  * chain c to a CSV file with the reference's "%i,%i,%f,..." formatting (and the
@@ -149,9 +152,10 @@ int nmc_debug_igamci(const double* a, const double* q, const double* lga, int n,
                      double* out);
 int nmc_debug_rng(const uint32_t* ctr5, int n, uint32_t seed, double gamma_shape,
                   double* out4);
-/* Diagnostic build only (make stamps -> libnestmc_stamps.so): per-workgroup phase
- * timestamps of the step kernel, [n_blocks][8] (100 MHz s_memrealtime).       */
-int nmc_debug_stamps(nmc_ctx* ctx, int n_blocks, uint64_t* out);
+/* Diagnostic build only (make stamps -> libnestmc_stamps.so): shader-clock phase
+ * stamps of the step kernel, [2 blocks][2 waves][8 iterations][16 slots]; n > 0
+ * arms (zeroes) the buffer, out != NULL copies it back.  Error in the shipped lib. */
+int nmc_debug_stamps(nmc_ctx* ctx, int n, uint64_t* out);
 
 #ifdef __cplusplus
 }

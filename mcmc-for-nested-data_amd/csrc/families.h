@@ -10,6 +10,8 @@
 //   finish() group log-likelihood from the accumulators and the row count
 //   obs_ll() one observation's log-likelihood in the reference's own formula
 //            (StepMethod.logLikelihood rows, posteriorSampling.py:656-659)
+//   gconst()/finish_fast() the same group LL with the per-group constant hoisted
+//            out of the decision's critical path (<= 1 ulp from finish())
 // Algebra is restructured (e.g. sum r^2 then scale once) but no fast-math: NaN and
 // inf propagate exactly as the reference's MH branches (:347-367) need.
 #pragma once
@@ -35,6 +37,7 @@ struct FamLinreg {
   int intercept;
   double sigma_known;   // > 0: fixed noise sd; else sigma is the last parameter
   double log_sigma_known;
+  double inv_s2_known;  // 1 / sigma_known^2
 
   struct Reg { double b0, b[K > 0 ? K : 1], sig; };
 
@@ -77,6 +80,17 @@ struct FamLinreg {
     const double ls = sigma_known > 0.0 ? log_sigma_known : log(s);
     return -0.5 * (acc[0] / (s * s)) - (double)n * (NMC_LOG_C + ls);
   }
+  // Per-group constant of finish_fast (once per launch): n (log sqrt(2 pi) + log sigma).
+  __device__ __forceinline__ double gconst(long n) const {
+    return sigma_known > 0.0 ? (double)n * (NMC_LOG_C + log_sigma_known) : 0.0;
+  }
+  // finish() on the decision's critical path: known sigma -> one multiply-add.
+  __device__ __forceinline__ double finish_fast(const Reg& r, const double* acc, long n,
+                                                double gc) const {
+    if (n == 0) return 0.0;
+    if (sigma_known > 0.0) return -0.5 * (acc[0] * inv_s2_known) - gc;
+    return finish(r, acc, n);
+  }
   __device__ __forceinline__ double obs_ll(const Reg& r, const double* __restrict__ row) const {
     double yh = 0.0;
     if (intercept) yh = r.b0;                        // numpy.sum(X * beta, axis=1)
@@ -101,6 +115,8 @@ struct FamGaussMean {
   static constexpr int NACC = NF;
   double sd[NF];
   double lsd[NF];   // log(sd_j), host (numpy) computed
+  double isd2[NF];  // 1 / sd_j^2
+  int bad;          // some sd_j <= 0: every group LL is NaN
 
   struct Reg { double t[NF]; };
 
@@ -138,6 +154,21 @@ struct FamGaussMean {
       out += -0.5 * (acc[j] / (sd[j] * sd[j])) - (double)n * (NMC_LOG_C + lsd[j]);
     }
     return out;
+  }
+  __device__ __forceinline__ double gconst(long n) const {
+    double c = 0.0;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) c += (double)n * (NMC_LOG_C + lsd[j]);
+    return c;
+  }
+  __device__ __forceinline__ double finish_fast(const Reg&, const double* acc, long n,
+                                                double gc) const {
+    if (n == 0) return 0.0;
+    if (bad) return nmc_nan();
+    double q = 0.0;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) q += -0.5 * (acc[j] * isd2[j]);
+    return q - gc;
   }
   __device__ __forceinline__ double obs_ll(const Reg& r, const double* __restrict__ row) const {
     double out = 0.0;
@@ -195,6 +226,11 @@ struct FamLogistic {
   }
   __device__ __forceinline__ double finish(const Reg&, const double* acc, long n) const {
     return n == 0 ? 0.0 : acc[0];
+  }
+  __device__ __forceinline__ double gconst(long) const { return 0.0; }
+  __device__ __forceinline__ double finish_fast(const Reg& r, const double* acc, long n,
+                                                double) const {
+    return finish(r, acc, n);
   }
   __device__ __forceinline__ double obs_ll(const Reg& r, const double* __restrict__ row) const {
     double eta = 0.0;

@@ -55,10 +55,15 @@ struct nmc_ctx {
   size_t kev_used = 0, hev_used = 0;
   double step_ms = 0, hyper_ms = 0;
   long long step_n = 0, hyper_n = 0;
-  int stamp_blocks = 0;
-  double* vbuf[2] = {nullptr, nullptr};   // value ping-pong ([P][G][C] each)
-  int vcur = 0;
+  long long step_iters = 0;
+  std::vector<int> kev_iters;             // iterations covered by each timed step launch
+  int cur_slot = 1;                       // values after the last iteration: vb[cur_slot]
+  int nacc = 1;                           // likelihood accumulators of the family
+  bool persistent = false;                // partial pooling: one resident launch per chunk
+  int ncu = 256;
 };
+
+static double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->d.vb0; }
 
 template <class T>
 static int dalloc(nmc_ctx* x, T** p, size_t n) {
@@ -85,12 +90,19 @@ static FamLinreg<NF> make_linreg(const std::vector<double>& c) {
   f.intercept = (int)c[1];
   f.sigma_known = c[2];
   f.log_sigma_known = c.size() > 3 ? c[3] : 0.0;
+  f.inv_s2_known = c[2] > 0 ? 1.0 / (c[2] * c[2]) : 0.0;
   return f;
 }
 template <int NF>
 static FamGaussMean<NF> make_gauss(const std::vector<double>& c) {
   FamGaussMean<NF> f{};
-  for (int j = 0; j < NF; ++j) { f.sd[j] = c[j]; f.lsd[j] = c[NF + j]; }
+  f.bad = 0;
+  for (int j = 0; j < NF; ++j) {
+    f.sd[j] = c[j];
+    f.lsd[j] = c[NF + j];
+    f.isd2[j] = 1.0 / (c[j] * c[j]);
+    if (!(c[j] > 0.0)) f.bad = 1;
+  }
   return f;
 }
 template <int NF>
@@ -126,19 +138,46 @@ static int with_family(nmc_ctx* x, Fn&& fn) {
   return fail(-1, "n_fields must be 1..9");
 }
 
-static int choose_waves(int CB, int G, int64_t n_obs) {
-  if (const char* e = getenv("NMC_WAVES")) {
-    int w = atoi(e);
-    if (w >= 1 && w <= 8) return w;
-  }
-  const int64_t wgs = (int64_t)CB * G;
-  int64_t w = (2048 + wgs - 1) / wgs;                 // ~8 waves per CU on 256 CUs
-  const int64_t navg = G > 0 ? n_obs / G : 0;
-  const int64_t wmax_rows = navg / 32 > 1 ? navg / 32 : 1;   // >= 32 rows per wave
-  if (w > wmax_rows) w = wmax_rows;
-  if (w > 8) w = 8;                 // nmc_k_iter launch bound: 512 threads
+static size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
+  const Dev& d = x->d;
+  return (size_t)nmc_lds(x->nacc, d.P, x->pooling == NMC_POOL_PARTIAL, d.nleaf, d.ntail, d.W,
+                         d.G, hlds, rows_lds ? d.nmax * x->nf : 0)
+             .total * 512;
+}
+static size_t run_lds_bytes(const nmc_ctx* x) {
+  return lds_bytes_for(x, x->persistent && x->d.hlds ? 1 : 0, x->d.rows_lds);
+}
+
+// Waves per workgroup from the rows per group only (>= 64 rows per likelihood wave,
+// at most 16): the likelihood partition -- and so every sum -- is then the same for
+// any chain count, launch mode or GPU count.  Partial pooling reserves NAUX waves at
+// step 0 for the Gibbs update (they compute it in persistent payload-in-LDS mode).
+static void choose_geometry(nmc_ctx* x) {
+  Dev& d = x->d;
+  int64_t w = 1 + (d.nmax + 63) / 64;
+  if (w > 16) w = 16;
   if (w < 1) w = 1;
-  return (int)w;
+  if (const char* e = getenv("NMC_WAVES")) {
+    const int v = atoi(e);
+    if (v >= 1 && v <= 16) w = v;
+  }
+  d.W = (int)w;
+  // partial pooling: NAUX = ceil(G / 32) (<= 4) auxiliary waves, one batch of 32
+  // loads each per Gibbs update; reserved in every partial mode so the likelihood
+  // partition (W - 1 - NAUX waves) is the same whatever the launch mode
+  d.naux = 0;
+  if (x->pooling == NMC_POOL_PARTIAL) {
+    const int na = (d.G + 31) / 32 < 4 ? (d.G + 31) / 32 : 4;
+    if (d.W >= na + 2 && d.G <= 128) d.naux = na;
+  }
+  // rows in LDS when they fit beside the rest of the carve (64 KiB for the rows)
+  d.rows_lds = (size_t)d.nmax * x->nf * 8 <= (size_t)64 * 1024 &&
+               lds_bytes_for(x, 0, 1) <= (size_t)96 * 1024 &&
+               !(getenv("NMC_NO_LDS_ROWS") && atoi(getenv("NMC_NO_LDS_ROWS")));
+  // the persistent Gibbs update by the auxiliary waves needs G <= 128 (one numpy
+  // leaf) and one parameter's chain-block values in LDS
+  d.hlds = d.naux > 0 && d.G <= 128 && lds_bytes_for(x, 1, d.rows_lds) <= (size_t)160 * 1024 &&
+           !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
 }
 
 static int pop_event_pair(nmc_ctx* x, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v,
@@ -153,48 +192,100 @@ static int pop_event_pair(nmc_ctx* x, std::vector<std::pair<hipEvent_t, hipEvent
   return 0;
 }
 
-static int nacc_of(const nmc_ctx* x) { return x->family == NMC_LL_GAUSS_MEAN ? x->nf : 1; }
+// numpy's pairwise-sum recursion over G groups (numpy/_core/src/umath/loops_utils.h):
+// leaves of <= 128 elements in order, and the post-order merges of their sums.
+static int pairwise_plan(int s, int n, std::vector<int>& starts, std::vector<int>& merges) {
+  if (n <= 128) {
+    starts.push_back(s);
+    return (int)starts.size() - 1;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  const int a = pairwise_plan(s, n2, starts, merges);
+  const int b = pairwise_plan(s + n2, n - n2, starts, merges);
+  merges.push_back(a);
+  merges.push_back(b);
+  return a;
+}
 
-// One launch per iteration: reads the current value buffer, writes the other one.
+static int run_mode(const nmc_ctx* x) {
+  if (x->pooling != NMC_POOL_PARTIAL) return NMC_MODE_NOPOOL;
+  if (!x->persistent) return NMC_MODE_LAUNCH;
+  return x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
+}
+
+// Iterations [i0, i1) of the step kernel (one launch).
 template <class Fam>
-static int launch_iter(nmc_ctx* x, const Fam& fam, int iter) {
+static int launch_run(nmc_ctx* x, const Fam& fam, int i0, int i1, int flags) {
   Dev& d = x->d;
-  const nmc_lds_layout L = nmc_lds(d.stage_rows, Fam::NFIELDS, d.W, Fam::NACC, d.P);
-  const size_t lds = (size_t)L.total * sizeof(double);
-  double* src = x->vbuf[x->vcur];
-  double* dst = x->vbuf[x->vcur ^ 1];
-  d.value = src;
+  const size_t lds = run_lds_bytes(x);
   std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
   if (x->ktiming) {
     if (int rc = pop_event_pair(x, x->kev, x->kev_used, &ev)) return rc;
+    if (x->kev_iters.size() < x->kev_used) x->kev_iters.resize(x->kev_used);
+    x->kev_iters[x->kev_used - 1] = i1 - i0;
     HIPCHK(hipEventRecord(ev->first, x->stream));
   }
-  if (d.stage_rows)
-    hipLaunchKernelGGL((nmc_k_iter<Fam, true>), dim3(d.CB * d.G), dim3(64 * d.W), lds,
-                       x->stream, d, fam, d.obs, (const double*)src, dst, iter);
-  else
-    hipLaunchKernelGGL((nmc_k_iter<Fam, false>), dim3(d.CB * d.G), dim3(64 * d.W), lds,
-                       x->stream, d, fam, d.obs, (const double*)src, dst, iter);
+  const dim3 grid(d.CB * d.G), block(64 * d.W);
+  switch (run_mode(x)) {
+    case NMC_MODE_NOPOOL:
+      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_NOPOOL>), grid, block, lds, x->stream, d, fam,
+                         d.obs, i0, i1, flags);
+      break;
+    case NMC_MODE_LAUNCH:
+      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_LAUNCH>), grid, block, lds, x->stream, d, fam,
+                         d.obs, i0, i1, flags);
+      break;
+    case NMC_MODE_SYNC:
+      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC>), grid, block, lds, x->stream, d, fam,
+                         d.obs, i0, i1, flags);
+      break;
+    default:
+      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC_LDS>), grid, block, lds, x->stream, d, fam,
+                         d.obs, i0, i1, flags);
+  }
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev->second, x->stream));
-  x->vcur ^= 1;
-  d.value = dst;
   return 0;
 }
 
-// Gibbs update of every parameter at iteration hiter (closes a chunk of iterations).
-static int launch_hyper(nmc_ctx* x, int hiter) {
+// Gibbs update after iteration t alone (closes a chunk in launch-per-iteration mode).
+static int launch_hyper(nmc_ctx* x, int t) {
   std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
   if (x->ktiming) {
     if (int rc = pop_event_pair(x, x->hev, x->hev_used, &ev)) return rc;
     HIPCHK(hipEventRecord(ev->first, x->stream));
   }
-  x->d.value = x->vbuf[x->vcur];
-  const size_t lds = (size_t)12 * x->P * 64 * sizeof(double);
-  hipLaunchKernelGGL(nmc_k_hyper, dim3(x->d.CB), dim3(64 * x->d.W), lds, x->stream, x->d,
-                     hiter);
+  const Dev& d = x->d;
+  const size_t lds = (size_t)nmc_lds(0, d.P, 1, d.nleaf, d.ntail, 0, d.G, 0).total * 512;
+  hipLaunchKernelGGL(nmc_k_hyper, dim3(d.CB), dim3(64 * d.W), lds, x->stream, x->d,
+                     (const double*)vslot(x, t & 1), t);
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev->second, x->stream));
+  return 0;
+}
+
+// Partial pooling: may every workgroup of the grid be resident at once?  (The
+// persistent kernel's chain-block waits need it.)  One block of margin per CU where
+// the occupancy query can over-report (MI355X_MICROARCH.md, residency).
+template <class Fam>
+static bool can_persist(nmc_ctx* x) {
+  if (const char* e = getenv("NMC_PERSIST")) return atoi(e) != 0;
+  int nb = 0;
+  const void* k = x->d.hlds ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_LDS>
+                            : (const void*)nmc_k_run<Fam, NMC_MODE_SYNC>;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W,
+                                                   lds_bytes_for(x, x->d.hlds, x->d.rows_lds)) !=
+      hipSuccess)
+    return false;
+  const int safe = nb > 1 ? nb - 1 : nb;
+  return (int64_t)x->d.CB * x->d.G <= (int64_t)safe * x->ncu;
+}
+
+static int check_timeout(nmc_ctx* x) {
+  unsigned t = 0;
+  HIPCHK(hipMemcpy(&t, x->d.tmo, sizeof(t), hipMemcpyDeviceToHost));
+  if (t) return fail(-5, "persistent kernel: a chain-block wait timed out (workgroups not resident?)");
   return 0;
 }
 
@@ -267,9 +358,8 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   rc |= dalloc(x, &dobs, (size_t)n_obs * n_fields);
   rc |= dalloc(x, &pf, n_params);
   rc |= dalloc(x, &pp, (size_t)8 * n_params);
-  rc |= dalloc(x, &x->vbuf[0], PGC);
-  rc |= dalloc(x, &x->vbuf[1], PGC);
-  d.value = x->vbuf[0];
+  rc |= dalloc(x, &d.vb0, PGC);
+  rc |= dalloc(x, &d.vb1, PGC);
   rc |= dalloc(x, &d.lp, PGC);
   rc |= dalloc(x, &d.ll, GC);
   rc |= dalloc(x, &d.scale, PGC);
@@ -285,20 +375,52 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   d.C = n_chains; d.G = n_groups; d.P = n_params; d.pooling = pooling; d.nf = n_fields;
   d.chain_base = chain_base; d.rng_mode = rng_mode; d.seed = seed;
   d.CB = (n_chains + 63) / 64;
-  d.W = choose_waves(d.CB, n_groups, n_obs);
   d.ha = (n_groups - 1) / 2.0;
   d.hlga = lgamma(d.ha > 0 ? d.ha : 1.0);
   {
-    // stage each group's rows in LDS when the whole workgroup carve fits 96 KiB
-    int64_t nmax = 0;
-    for (int g = 0; g < n_groups; ++g)
-      nmax = std::max<int64_t>(nmax, group_offsets[g + 1] - group_offsets[g]);
-    const int nacc = ll_family == NMC_LL_GAUSS_MEAN ? n_fields : 1;
-    const nmc_lds_layout L = nmc_lds((int)std::min<int64_t>(nmax, 1 << 20), n_fields, d.W,
-                                     nacc, n_params);
-    d.stage_rows = ((size_t)L.total * 8 <= (size_t)96 * 1024 && !getenv("NMC_NO_STAGE"))
-                       ? (int)nmax : 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+      x->ncu = prop.multiProcessorCount;
   }
+  x->nacc = ll_family == NMC_LL_GAUSS_MEAN ? n_fields : 1;
+  // numpy pairwise-sum plan of the hyper update (partial pooling)
+  std::vector<int> starts, merges;
+  pairwise_plan(0, n_groups, starts, merges);
+  int ntail = 0;
+  for (size_t k = 0; k < starts.size(); ++k) {
+    const int m = (k + 1 < starts.size() ? starts[k + 1] : n_groups) - starts[k];
+    const int m8 = m >= 8 ? m - m % 8 : 0;
+    ntail = std::max(ntail, m - m8);
+  }
+  starts.push_back(n_groups);
+  d.nleaf = (int)starts.size() - 1;
+  d.nmerge = (int)merges.size() / 2;
+  d.ntail = ntail;
+  int* dleaf = nullptr;
+  int* dmerge = nullptr;
+  rc |= dalloc(x, &dleaf, starts.size());
+  rc |= dalloc(x, &dmerge, merges.size());
+  rc |= dalloc(x, &d.cnt, (size_t)32 * d.CB * n_params);
+  rc |= dalloc(x, &d.tmo, 4);
+  if (rc) { nmc_destroy(x); return rc; }
+  d.leaf = dleaf;
+  d.merge = dmerge;
+  HIPCHK(hipMemcpy(dleaf, starts.data(), starts.size() * sizeof(int), hipMemcpyHostToDevice));
+  if (!merges.empty())
+    HIPCHK(hipMemcpy(dmerge, merges.data(), merges.size() * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(d.tmo, 0, 16));
+  int64_t nmax = 0;
+  for (int g = 0; g < n_groups; ++g)
+    nmax = std::max<int64_t>(nmax, group_offsets[g + 1] - group_offsets[g]);
+  d.nmax = (int)nmax;
+  choose_geometry(x);
+  if (run_lds_bytes(x) > (size_t)160 * 1024) {
+    nmc_destroy(x);
+    return fail(-1, "workgroup state exceeds the 160 KiB LDS of a CU (too many parameters, "
+                    "groups or rows per group)");
+  }
+  if (pooling == NMC_POOL_PARTIAL)
+    x->persistent = with_family(x, [&](auto fam) -> int { return can_persist<decltype(fam)>(x) ? 1 : 0; }) == 1;
   d.thin = 1; d.tune_interval = 100;
   HIPCHK(hipMemcpy(off, group_offsets, (n_groups + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
   if (n_obs > 0)
@@ -332,7 +454,8 @@ int nmc_set_state(nmc_ctx* x, const double* value, const double* log_prior, cons
   hipSetDevice(x->device);
   Dev& d = x->d;
   const size_t PGC = (size_t)x->P * x->G * x->C, GC = (size_t)x->G * x->C, PC = (size_t)x->P * x->C;
-  HIPCHK(hipMemcpy(d.value, value, PGC * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d.vb1, value, PGC * 8, hipMemcpyHostToDevice));
+  x->cur_slot = 1;
   HIPCHK(hipMemcpy(d.lp, log_prior, PGC * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d.ll, ll, GC * 8, hipMemcpyHostToDevice));
   if (x->pooling == NMC_POOL_PARTIAL) {
@@ -362,7 +485,7 @@ int nmc_get_state(nmc_ctx* x, double* value, double* log_prior, double* ll, doub
   HIPCHK(hipStreamSynchronize(x->stream));
   Dev& d = x->d;
   const size_t PGC = (size_t)x->P * x->G * x->C, GC = (size_t)x->G * x->C, PC = (size_t)x->P * x->C;
-  if (value) HIPCHK(hipMemcpy(value, d.value, PGC * 8, hipMemcpyDeviceToHost));
+  if (value) HIPCHK(hipMemcpy(value, vslot(x, x->cur_slot), PGC * 8, hipMemcpyDeviceToHost));
   if (log_prior) HIPCHK(hipMemcpy(log_prior, d.lp, PGC * 8, hipMemcpyDeviceToHost));
   if (ll) HIPCHK(hipMemcpy(ll, d.ll, GC * 8, hipMemcpyDeviceToHost));
   if (hyper_mu) HIPCHK(hipMemcpy(hyper_mu, d.mu, PC * 8, hipMemcpyDeviceToHost));
@@ -421,10 +544,9 @@ int nmc_set_schedule(nmc_ctx* x, int n_iter, int burn, int thin, int tune_interv
   int vcap = (int)(budget / per_iter);
   if (vcap < 1) vcap = 1;
   if (vcap > n_iter) vcap = n_iter > 0 ? n_iter : 1;
-  dfree(x, d.vz); dfree(x, d.vlu); dfree(x, d.vhz); dfree(x, d.vhx);
+  dfree(x, d.vzl); dfree(x, d.vh);
   const size_t PGC = (size_t)x->P * x->G * x->C, PC = (size_t)x->P * x->C;
-  rc = dalloc(x, &d.vz, vcap * PGC) | dalloc(x, &d.vlu, vcap * PGC) |
-       dalloc(x, &d.vhz, vcap * PC) | dalloc(x, &d.vhx, vcap * PC);
+  rc = dalloc(x, &d.vzl, 2 * vcap * PGC) | dalloc(x, &d.vh, 2 * vcap * PC);
   if (rc) return rc;
   d.vcap = vcap;
   d.vbase = 0;
@@ -464,7 +586,14 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
     return fail(-1, "replay variates do not cover the iteration range");
   const bool partial = x->pooling == NMC_POOL_PARTIAL;
   const int P = x->P;
-  return with_family(x, [&](auto fam) -> int {
+  // the kernels read the values after iteration iter_begin-1 from vb[(iter_begin-1)&1]
+  const int need = (iter_begin - 1) & 1;
+  if (x->cur_slot != need) {
+    HIPCHK(hipMemcpyAsync(vslot(x, need), vslot(x, x->cur_slot),
+                          (size_t)x->P * x->G * x->C * 8, hipMemcpyDeviceToDevice, x->stream));
+    x->cur_slot = need;
+  }
+  int rc = with_family(x, [&](auto fam) -> int {
     for (int c0 = iter_begin; c0 < iter_end; c0 += x->d.vcap) {
       const int c1 = c0 + x->d.vcap < iter_end ? c0 + x->d.vcap : iter_end;
       // every variate of iterations [c0, c1) in one fully parallel launch
@@ -473,20 +602,28 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);
       hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);
       HIPCHK(hipGetLastError());
-      for (int it = c0; it < c1; ++it)
-        if (int rc = launch_iter(x, fam, it)) return rc;
-      // close the chunk: the last Gibbs update reads this chunk's variates
-      if (partial)
-        if (int rc = launch_hyper(x, c1 - 1)) return rc;
+      if (!partial) {
+        if (int rc = launch_run(x, fam, c0, c1, 0)) return rc;
+      } else if (x->persistent) {
+        HIPCHK(hipMemsetAsync(x->d.cnt, 0, (size_t)32 * x->d.CB * x->P * sizeof(unsigned),
+                              x->stream));
+        if (int rc = launch_run(x, fam, c0, c1, NMC_RUN_HYPER_LOAD)) return rc;
+      } else {
+        for (int it = c0; it < c1; ++it)
+          if (int rc = launch_run(x, fam, it, it + 1, it == c0 ? NMC_RUN_HYPER_LOAD : 0)) return rc;
+        if (int rc = launch_hyper(x, c1 - 1)) return rc;   // closes the chunk
+      }
     }
     return 0;
   });
+  x->cur_slot = (iter_end - 1) & 1;
+  return rc;
 }
 
 int nmc_synchronize(nmc_ctx* x) {
   hipSetDevice(x->device);
   HIPCHK(hipStreamSynchronize(x->stream));
-  return 0;
+  return check_timeout(x);
 }
 
 int nmc_get_samples(nmc_ctx* x, int row_begin, int n_rows, double* out) {
@@ -495,6 +632,7 @@ int nmc_get_samples(nmc_ctx* x, int row_begin, int n_rows, double* out) {
   if (row_begin < 0 || n_rows < 0 || row_begin + n_rows > d.n_rows)
     return fail(-1, "row range out of bounds");
   HIPCHK(hipStreamSynchronize(x->stream));
+  if (int rc = check_timeout(x)) return rc;
   const size_t per = (size_t)d.cols * x->C;
   if (n_rows)
     HIPCHK(hipMemcpy(out, d.samples + (size_t)row_begin * per, (size_t)n_rows * per * 8,
@@ -542,7 +680,7 @@ int nmc_eval_obs_ll(nmc_ctx* x, double* out) {
   int rc = with_family(x, [&](auto fam) -> int {
     using F = decltype(fam);
     hipLaunchKernelGGL(nmc_k_obs_ll<F>, dim3(x->d.CB * x->G), dim3(64), 0, x->stream, x->d,
-                       fam, o, x->n_obs);
+                       fam, (const double*)vslot(x, x->cur_slot), o, x->n_obs);
     HIPCHK(hipGetLastError());
     return 0;
   });
@@ -575,11 +713,12 @@ int nmc_set_kernel_timing(nmc_ctx* x, int enable) {
   x->kev_used = x->hev_used = 0;
   x->step_ms = x->hyper_ms = 0;
   x->step_n = x->hyper_n = 0;
+  x->step_iters = 0;
   return 0;
 }
 
-int nmc_get_kernel_timing(nmc_ctx* x, double* step_ms, int64_t* step_n, double* hyper_ms,
-                          int64_t* hyper_n) {
+int nmc_get_kernel_timing(nmc_ctx* x, double* step_ms, int64_t* step_n, int64_t* step_iters,
+                          double* hyper_ms, int64_t* hyper_n) {
   hipSetDevice(x->device);
   HIPCHK(hipStreamSynchronize(x->stream));
   for (size_t i = 0; i < x->kev_used; ++i) {
@@ -587,6 +726,7 @@ int nmc_get_kernel_timing(nmc_ctx* x, double* step_ms, int64_t* step_n, double* 
     HIPCHK(hipEventElapsedTime(&ms, x->kev[i].first, x->kev[i].second));
     x->step_ms += ms;
     x->step_n += 1;
+    x->step_iters += x->kev_iters[i];
   }
   for (size_t i = 0; i < x->hev_used; ++i) {
     float ms = 0;
@@ -597,14 +737,16 @@ int nmc_get_kernel_timing(nmc_ctx* x, double* step_ms, int64_t* step_n, double* 
   x->kev_used = x->hev_used = 0;
   if (step_ms) *step_ms = x->step_ms;
   if (step_n) *step_n = x->step_n;
+  if (step_iters) *step_iters = x->step_iters;
   if (hyper_ms) *hyper_ms = x->hyper_ms;
   if (hyper_n) *hyper_n = x->hyper_n;
   return 0;
 }
 
-int nmc_launch_config(nmc_ctx* x, int* waves_per_group, int* chain_blocks) {
+int nmc_launch_config(nmc_ctx* x, int* waves_per_group, int* chain_blocks, int* persistent) {
   *waves_per_group = x->d.W;
   *chain_blocks = x->d.CB;
+  if (persistent) *persistent = x->persistent || x->pooling != NMC_POOL_PARTIAL ? 1 : 0;
   return 0;
 }
 
@@ -733,23 +875,23 @@ int nmc_debug_prior_logpdf(int fam, const double* prm8, const double* xs, int n,
   return 0;
 }
 
-int nmc_debug_stamps(nmc_ctx* x, int n_blocks, uint64_t* out) {
-  // n_blocks > 0: (re)allocate and zero [n_blocks][8]; out != NULL: copy back.
+// Diagnostic build only: (re)allocate and zero the stamp buffer (n > 0) and/or copy
+// it back (out != NULL); [2 blocks][2 waves][8 iterations][16 slots] shader clocks.
+int nmc_debug_stamps(nmc_ctx* x, int n, uint64_t* out) {
+#ifdef NMC_STAMPS
   hipSetDevice(x->device);
-  if (n_blocks > 0) {
-    dfree(x, x->d.stamps);
-    x->d.stamps = nullptr;
-    if (int rc = dalloc(x, &x->d.stamps, (size_t)n_blocks * 8)) return rc;
-    HIPCHK(hipMemset(x->d.stamps, 0, (size_t)n_blocks * 64));
-    x->stamp_blocks = n_blocks;
+  if (n > 0) {
+    if (!x->d.stamps)
+      if (int rc = dalloc(x, &x->d.stamps, 512)) return rc;
+    HIPCHK(hipMemset(x->d.stamps, 0, 512 * 8));
   }
   if (out) {
     HIPCHK(hipStreamSynchronize(x->stream));
-    HIPCHK(hipMemcpy(out, x->d.stamps, (size_t)x->stamp_blocks * 64, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out, x->d.stamps, 512 * 8, hipMemcpyDeviceToHost));
   }
-#ifdef NMC_STAMPS
   return 0;
 #else
+  (void)x; (void)n; (void)out;
   return fail(-1, "not a stamps build (make stamps)");
 #endif
 }

@@ -30,6 +30,15 @@ __device__ __forceinline__ double nmc_norm_logpdf(double x, double loc, double s
   return (-(y * y) / 2.0 - NMC_LOG_C) - lsd;
 }
 
+// The same with the reciprocal of the scale precomputed (isd = 1/scale; <= 1 ulp
+// from the division form): the partial-pooling priors on the decision's path.
+__device__ __forceinline__ double nmc_norm_logpdf_r(double x, double loc, double scale,
+                                                    double isd, double lsd) {
+  const double y = (x - loc) * isd;
+  if (!(scale > 0.0) || isnan(y)) return nmc_nan();
+  return (-(y * y) / 2.0 - NMC_LOG_C) - lsd;
+}
+
 __device__ __forceinline__ double nmc_xlogy(double c, double y) {
   if (c == 0.0 && !isnan(y)) return 0.0;
   return c * log(y);

@@ -179,13 +179,15 @@ class Engine:
 
     def kernel_timing(self):
         sm, hm = ctypes.c_double(), ctypes.c_double()
-        sn, hn = ctypes.c_int64(), ctypes.c_int64()
+        sn, si, hn = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         check(self.lib.nmc_get_kernel_timing(self.h, ctypes.byref(sm), ctypes.byref(sn),
-                                             ctypes.byref(hm), ctypes.byref(hn)))
-        return dict(step_ms=sm.value, step_launches=sn.value, hyper_ms=hm.value,
-                    hyper_launches=hn.value)
+                                             ctypes.byref(si), ctypes.byref(hm),
+                                             ctypes.byref(hn)))
+        return dict(step_ms=sm.value, step_launches=sn.value, step_iters=si.value,
+                    hyper_ms=hm.value, hyper_launches=hn.value)
 
     def launch_config(self):
-        w, cb = ctypes.c_int(), ctypes.c_int()
-        check(self.lib.nmc_launch_config(self.h, ctypes.byref(w), ctypes.byref(cb)))
-        return dict(waves_per_group=w.value, chain_blocks=cb.value)
+        w, cb, pe = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(self.lib.nmc_launch_config(self.h, ctypes.byref(w), ctypes.byref(cb),
+                                         ctypes.byref(pe)))
+        return dict(waves_per_group=w.value, chain_blocks=cb.value, persistent=bool(pe.value))

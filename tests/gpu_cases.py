@@ -50,6 +50,10 @@ def synthetic(kind, C, G, N, seed=3, ragged=False):
         fam = GaussianMean.from_groups(mu, sd, sizes)
         priors = [scipy.stats.norm(0, 1)] * 3
         return fam, sizes, priors, "none", ("a", "b", "c")
+    if kind == "gauss1_partial":
+        mu = rs.normal(size=(1, G))
+        fam = GaussianMean.from_groups(mu, [0.8], sizes)
+        return fam, sizes, None, "partial", ("a",)
     if kind == "logistic_partial":
         K = 4
         X = numpy.hstack([numpy.ones((n, 1)), rs.normal(size=(n, K - 1))])

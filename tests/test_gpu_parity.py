@@ -75,6 +75,12 @@ def _synthetic_state(fam, sizes, priors, pooling, C, P, G, seed=5):
     ("regression3_none", 65, 4, 25, False, 150),
     ("gauss_none", 64, 6, 20, True, 80),
     ("linreg_complete", 3, 1, 300, False, 250),
+    # persistent launch, Gibbs update by auxiliary waves from LDS (W = 5, NAUX = 2)
+    ("linreg_partial", 64, 64, 256, False, 24),
+    # persistent launch, Gibbs update by auxiliary waves, ragged rows
+    ("logistic_partial", 96, 24, 200, True, 16),
+    # one parameter: the auxiliary update and the decision share a step
+    ("gauss1_partial", 64, 40, 256, False, 30),
 ])
 def test_philox_matches_oracle(gpu_lib, kind, C, G, N, ragged, n_iter):
     fam, sizes, priors, pooling, names = synthetic(kind, C, G, N, ragged=ragged)

@@ -20,7 +20,11 @@ from nestmc.engine import Engine  # noqa: E402
 from nestmc.families import LinearRegression, Logistic, GaussianMean  # noqa: E402
 
 
-def engine_for(kind, C, G, N, pooling, waves):
+def engine_for(kind, C, G, N, pooling, waves, persist=None):
+    if persist is None:
+        os.environ.pop("NMC_PERSIST", None)
+    else:
+        os.environ["NMC_PERSIST"] = str(int(persist))
     if waves:
         os.environ["NMC_WAVES"] = str(waves)
     else:
@@ -54,8 +58,8 @@ def engine_for(kind, C, G, N, pooling, waves):
     return eng, fam
 
 
-def run(kind, C, G, N, pooling, waves, iters):
-    eng, fam = engine_for(kind, C, G, N, pooling, waves)
+def run(kind, C, G, N, pooling, waves, iters, persist=None):
+    eng, fam = engine_for(kind, C, G, N, pooling, waves, persist)
     eng.set_schedule(3 * iters, 3 * iters, 1)
     eng.run(0, iters)
     eng.synchronize()
@@ -73,8 +77,9 @@ def run(kind, C, G, N, pooling, waves, iters):
     eng.close()
     rate = C * G * iters / (ms / 1e3)
     return dict(kind=kind, C=C, G=G, N=N, pooling=pooling, waves=cfg["waves_per_group"],
+                persistent=cfg["persistent"],
                 us_per_iter=ms * 1e3 / iters, wall_us_per_iter=wall * 1e6 / iters,
-                step_us=kt["step_ms"] * 1e3 / max(1, kt["step_launches"]),
+                step_us_per_iter=kt["step_ms"] * 1e3 / max(1, kt["step_iters"]),
                 hyper_us=kt["hyper_ms"] * 1e3 / max(1, kt["hyper_launches"]),
                 rate=rate)
 
@@ -83,9 +88,21 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=300)
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--sweep", action="store_true", help="rows-per-group sweep (cost model)")
     a = ap.parse_args()
-    cases = [("linreg", 256, 64, 1000, "partial", w) for w in (0, 2, 4, 8)]
-    cases += [("linreg", 256, 64, 1000, "none", w) for w in (0, 4, 8)]
+    if a.sweep:
+        for rows in ("lds", "smem"):
+            if rows == "smem":
+                os.environ["NMC_NO_LDS_ROWS"] = "1"
+            for pooling in ("none", "partial"):
+                for N in (250, 1000, 2000, 4000):
+                    r = run("linreg", 256, 64, N, pooling, 16, a.iters)
+                    r["rows"] = rows
+                    print(json.dumps(r), flush=True)
+            os.environ.pop("NMC_NO_LDS_ROWS", None)
+        return
+    cases = [("linreg", 256, 64, 1000, "partial", w) for w in (0, 4, 8, 16)]
+    cases += [("linreg", 256, 64, 1000, "none", w) for w in (0, 8)]
     if not a.quick:
         cases += [("linreg", 1024, 256, 2000, "partial", 0),
                   ("gauss", 256, 32, 500, "none", 0),
@@ -93,6 +110,9 @@ def main():
     for c in cases:
         iters = a.iters if c[3] * c[1] * c[2] < 5e7 else max(20, a.iters // 10)
         print(json.dumps(run(*c, iters)), flush=True)
+    # launch-per-iteration partial pooling (the non-resident fallback)
+    print(json.dumps(run("linreg", 256, 64, 1000, "partial", 0, a.iters, persist=False)),
+          flush=True)
 
 
 if __name__ == "__main__":
