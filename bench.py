@@ -132,6 +132,10 @@ def main():
     # schedule: record the second half like the reference (burn = n_iter // 2)
     eng.set_schedule(n_iter, n_iter // 2, 1)
 
+    # every launch covers the same number of iterations (the warmup length), so the
+    # per-launch average below and rocprof's kernel average describe the same launch
+    LAUNCH_ITERS = max(1, W)
+    eng.set_launch_iters(LAUNCH_ITERS)
     # warmup (untimed)
     eng.run(0, W)
     eng.synchronize()
@@ -176,20 +180,26 @@ def main():
     value = units / t_max
     launches = kt["step_launches"]
     avg_step_ms = kt["step_ms"] / max(1, launches)
+    iters_per_launch = kt["step_iters"] / max(1, launches)
     b_obs = fam.bytes_per_obs()
-    # one launch = one iteration = P parameter steps; SURVEY 8(d): B_unit = P*N*b_obs
-    # per chain*group*iteration (each step streams the group's rows once per chain)
-    bytes_per_launch = C * G * P * N * b_obs
+    # B_unit = P*N*b_obs per chain*group*iteration (each parameter step
+    # evaluates the group's rows once per chain); a launch covers iters_per_launch
+    # iterations (persistent: a whole variate chunk)
+    bytes_per_launch = C * G * P * N * b_obs * iters_per_launch
     achieved_gbs = bytes_per_launch / (avg_step_ms * 1e-3) / 1e9
-    flops_per_launch = C * G * P * N * 5          # fma + sub + fma per (chain, obs, step)
+    # fp64 work: fma + sub + fma = 5 flops per (chain, obs, parameter step)
+    flops_per_launch = C * G * P * N * 5 * iters_per_launch
     fp64_tflops = flops_per_launch / (avg_step_ms * 1e-3) / 1e12
     traffic = None
     tfile = os.path.join(ROOT, "profiles", "hbm_traffic_r01.json")
     if os.path.exists(tfile):
-        try:
-            traffic = json.load(open(tfile)).get("bytes_per_step_launch")
+        try:   # PMC bytes per iteration of this workload (tools/hbm_traffic.py), per launch
+            traffic = json.load(open(tfile))["bytes_per_iteration"] * iters_per_launch
         except Exception:
             traffic = None
+    lc = eng.launch_config()
+    kname = "nmc_k_run<FamLinreg<2>, %s>" % (
+        "NMC_MODE_SYNC_LDS" if lc["persistent"] else "NMC_MODE_LAUNCH")
 
     if rank == 0:
         cpu = None
@@ -215,13 +225,17 @@ def main():
                                    "%d chains x %d groups x %d obs per GPU, P=%d" % (C, G, N, P),
                        "chains_per_gpu": C, "groups": G, "obs_per_group": N, "params": P,
                        "pooling": "partial", "parallelism": "chains sharded x%d" % world,
-                       "launch": eng.launch_config()},
+                       "launch": lc},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "kernel": "nmc_k_iter<FamLinreg<2>, true>",
+                         "kernel": kname,
                          "avg_launch_us": avg_step_ms * 1e3,
+                         "iterations_per_launch": iters_per_launch,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "note": "rows are LDS-resident for the whole launch, so the "
+                                 "algorithmic bytes exceed HBM: frac > 1 is expected; the "
+                                 "kernel's real bound is fp64 VALU issue (fp64_valu)",
                          "fp64_valu": {"achieved": fp64_tflops, "peak": FP64_VALU_PEAK_TFLOPS,
                                        "unit": "TFLOP/s",
                                        "frac": fp64_tflops / FP64_VALU_PEAK_TFLOPS}},

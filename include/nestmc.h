@@ -119,6 +119,9 @@ int nmc_event_elapsed(nmc_ctx* ctx, int slot_a, int slot_b, float* ms);
 int nmc_set_kernel_timing(nmc_ctx* ctx, int enable);
 int nmc_get_kernel_timing(nmc_ctx* ctx, double* step_ms_total, int64_t* step_launches,
                           int64_t* step_iters, double* hyper_ms_total, int64_t* hyper_launches);
+/* Cap the iterations one persistent launch covers (0 = the variate chunk, the
+ * default); e.g. equal-length launches for profiling.                           */
+int nmc_set_launch_iters(nmc_ctx* ctx, int max_iters);
 /* Launch geometry: waves per workgroup, 64-chain blocks, and whether one resident
  * launch runs a whole chunk of iterations (1) or one launch per iteration (0).   */
 int nmc_launch_config(nmc_ctx* ctx, int* waves_per_group, int* chain_blocks, int* persistent);

@@ -70,6 +70,7 @@ struct Dev {
   int nleaf, nmerge, ntail;
   int nmax;              // rows of the largest group
   int hlds, naux;        // persistent partial: Gibbs payload via LDS, auxiliary waves
+  int noprio;            // diagnostics: no issue priority for the latency-bound waves
   int rows_lds;          // 1: each workgroup stages its group's rows in LDS once per launch
   unsigned* cnt;         // [CB][P][32] publish counters (persistent partial), zeroed per launch
   unsigned* tmo;         // timeout word (persists; host checks it)
@@ -225,23 +226,26 @@ __host__ __device__ inline nmc_lds_layout nmc_lds(int nacc, int P, int partial, 
   nmc_lds_layout L;
   L.th = 0;
   L.part = L.th + P;
-  L.st = L.part + nacc * W;
+  L.st = L.part + nacc * 16;   // 16 partial slots per accumulator (unused: -0.0)
   L.hyp = L.st + 5 * P;
   L.hval = L.hyp + (partial ? 6 * P : 0);
-  L.hst = L.hval + (partial && hlds ? G : 0);
+  L.hst = L.hval + (partial && hlds ? 2 * G : 0);   // two task buffers
   L.hleaf = L.hst + (partial ? P * nleaf * (8 + ntail) : 0);
   L.zl = L.hleaf + (partial ? P * nleaf : 0);
   L.hv = L.zl + 4;
   L.cw = L.hv + (partial ? 2 * P : 0);
-  L.flag = L.cw + 12;
+  L.flag = L.cw + 15;
   L.rows = L.flag + 1;
   L.total = L.rows + (row_doubles + 63) / 64;
   return L;
 }
 enum { NMC_ST_S = 0, NMC_ST_LP, NMC_ST_NA, NMC_ST_NR, NMC_ST_TA };
 enum { NMC_HY_MU = 0, NMC_HY_SD, NMC_HY_LSD, NMC_HY_S2, NMC_HY_SDM, NMC_HY_ISD };
+// (PAC, PLP, PLL: the decided step's accept flag, log prior and log-likelihood, applied
+// to the state by the control wave at the next step, off the critical path)
 enum { NMC_CW_LU = 0, NMC_CW_LPC, NMC_CW_LPP, NMC_CW_PROP, NMC_CW_SA, NMC_CW_SR, NMC_CW_NAA,
-       NMC_CW_NRA, NMC_CW_NAR, NMC_CW_NRR, NMC_CW_TA, NMC_CW_V };
+       NMC_CW_NRA, NMC_CW_NAR, NMC_CW_NRR, NMC_CW_TA, NMC_CW_V, NMC_CW_PAC, NMC_CW_PLP,
+       NMC_CW_PLL };
 
 // Where the Gibbs update reads the published values: global (plain loads after a
 // kernel boundary / sc1 loads in a persistent launch) or the LDS copy the
@@ -462,7 +466,7 @@ __device__ __forceinline__ double nmc_leaf_sum(const double* v, int n, double mu
 // each) -> LDS hval, sc1 loads, 32 in flight.
 __device__ __forceinline__ void nmc_hyper_load(const Dev& d, const double* src, int p, int cc,
                                                int kb, int ke, double* lds,
-                                               const nmc_lds_layout& L) {
+                                               const nmc_lds_layout& L, int hoff) {
   const int lane = threadIdx.x & 63;
   const int C = d.C;
   src += (size_t)p * d.G * C;
@@ -473,7 +477,7 @@ __device__ __forceinline__ void nmc_hyper_load(const Dev& d, const double* src, 
       tv[u] = k0 + u < ke ? nmc_ldv<NMC_SRC_SC1>(src + (size_t)(k0 + u) * C + cc) : 0.0;
 #pragma unroll
     for (int u = 0; u < 32; ++u)
-      if (k0 + u < ke) lds[(size_t)(L.hval + k0 + u) * 64 + lane] = tv[u];
+      if (k0 + u < ke) lds[(size_t)(L.hval + hoff + k0 + u) * 64 + lane] = tv[u];
   }
 }
 
@@ -482,11 +486,11 @@ __device__ __forceinline__ void nmc_hyper_load(const Dev& d, const double* src, 
 // variates of (t, p).  Writes the LDS hyp columns of p (and, if write, global + row).
 __device__ __forceinline__ void nmc_hyper_compute(const Dev& d, int cb, int t, int p, double* lds,
                                                   const nmc_lds_layout& L, bool write, double hz,
-                                                  double hx) {
+                                                  double hx, int hoff) {
   const int lane = threadIdx.x & 63;
   const int P = d.P, G = d.G, C = d.C;
   const int c = cb * 64 + lane;
-  const double* hv = lds + (size_t)L.hval * 64 + lane;      // hv[i * 64]: group i of p
+  const double* hv = lds + (size_t)(L.hval + hoff) * 64 + lane;   // hv[i * 64]: group i of p
   double* hy = lds + L.hyp * 64 + lane;
   const double sdm = sqrt(hy[(NMC_HY_S2 * P + p) * 64] / G);
   const double tot = nmc_leaf_sum<false>(hv, G, 0.0);
@@ -688,6 +692,9 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const size_t PGC = (size_t)P * G * C;
   const size_t gc = (size_t)g * C + cc;
   const bool ctl = w == 0;
+  // latency-bound roles (control, loaders, compute) issue ahead of the likelihood waves
+  // sharing their SIMD, which fill the gaps
+  if (W > 1 && w <= naux && !(d.noprio)) __builtin_amdgcn_s_setprio(3);
 
   // ---- prologue: values and state -> LDS (parameter p by wave p % W) ----
   const double* vin = ((i0 - 1) & 1) ? d.vb1 : d.vb0;
@@ -719,8 +726,12 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   auto zl_src = [&](int tn, int pn) -> const double* {
     return d.vzl + ((size_t)(tn - d.vbase) * PGC + (size_t)pn * G * C + gc) * 2;
   };
+  const int l0 = W == 1 ? 0 : 1 + naux;   // likelihood waves l0..W-1
+  const int nll = W - l0;
   if (ctl) {     // {z, log u} of the first step -> LDS slot of step i0*P
     nmc_dma16(zl_src(i0, 0), lds + (L.zl + 2 * ((i0 * P) & 1)) * 64);
+    for (int j = 0; j < Fam::NACC; ++j)   // x + (-0.0) == x: the fixed 16-slot sum
+      for (int k = nll; k < 16; ++k) lds[(L.part + j * 16 + k) * 64 + lane] = -0.0;
     nmc_drain_vm();
     lds[L.flag * 64 + lane] = 0.0;
   }
@@ -728,31 +739,78 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
 
   bool ok = true;
   int pub_p = -1;     // control wave: parameter whose sc1 value store awaits its counter add
+  int pend_p = -1, pend_t = 0;   // control wave: decided step whose state update is pending
+  double* cwv = lds + L.cw * 64 + lane;    // cwv[k * 64]
+  // the rest of a decided step's state update (:369-383, :608-610): counters, log prior,
+  // log-likelihood, sample and trace rows
+  auto apply_pending = [&]() {
+    const int q = pend_p, tq = pend_t;
+    const bool accept = cwv[NMC_CW_PAC * 64] != 0.0;
+    const double llp = cwv[NMC_CW_PLL * 64];
+    st[(NMC_ST_LP * P + q) * 64] = cwv[NMC_CW_PLP * 64];
+    st[(NMC_ST_NA * P + q) * 64] = cwv[(accept ? NMC_CW_NAA : NMC_CW_NAR) * 64];
+    st[(NMC_ST_NR * P + q) * 64] = cwv[(accept ? NMC_CW_NRA : NMC_CW_NRR) * 64];
+    st[(NMC_ST_TA * P + q) * 64] = cwv[NMC_CW_TA * 64] + (accept ? 1.0 : 0.0);
+    if (accept) LL = llp;
+    if (live) {
+      const int row = nmc_record_row(d, tq);
+      if (row >= 0) {
+        const int col = q * (G + (PARTIAL ? 2 : 0)) + (PARTIAL ? 2 : 0) + g;
+        d.samples[((size_t)row * d.cols + col) * C + c] = th[q * 64];
+      }
+      if (tq < d.trace_n) {
+        const size_t it = (((size_t)tq * P + q) * G + g) * C + c;
+        d.tflag[it] = accept ? 1 : 0;
+        d.tllp[it] = llp;
+      }
+    }
+    pend_p = -1;
+  };
   for (int t = i0; t < i1 && ok; ++t) {
     NMC_STAMP(t, 0);
-    const int row_rec = nmc_record_row(d, t);
     const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
     for (int p = 0; p < P; ++p) {
       const int sp = (t * P + p) & 1;
       // Gibbs update of every parameter at step 0 (launch-per-iteration / fallback)
       const bool hyper_now =
           !hl && PARTIAL && p == 0 && t > 0 && !(t == i0 && (flags & NMC_RUN_HYPER_LOAD));
-      // payload-in-LDS: at step p the auxiliary waves update parameter q = p-1 (mod P)
-      // after iteration tq -- published by every workgroup right after its decision
-      const int aq = p > 0 ? p - 1 : P - 1;
+      // payload-in-LDS: the Gibbs update of parameter q after iteration tq is task
+      // k = tq*P + q; every workgroup publishes it right after its decision at global step
+      // k, so it is counted at the start of step k+1.  P == 1: the auxiliary waves load and
+      // compute task gs-1 at step gs (needed at once).  P >= 2 (two-stage pipeline): the
+      // loader waves copy task gs-1 into LDS buffer (gs-1)&1 at step gs, the compute wave
+      // updates task gs-2 from buffer gs&1 -- needed first at step gs-2+P.
+      const int gs = t * P + p, gs0 = i0 * P;
+      const bool pipe = hl && P >= 2;
+      const int aq = p > 0 ? p - 1 : P - 1;        // loaders' task: (atq, aq) = gs-1
       const int atq = p > 0 ? t : t - 1;
-      const bool aux_now = hl && atq >= i0;
+      const bool aux_now = hl && gs - 1 >= gs0;
+      const bool comp_now = pipe && gs - 2 >= gs0;  // compute wave's task: (ctq, cq) = gs-2
+      const int cq = (p + 2 * P - 2) % (P > 0 ? P : 1);
+      const int ctq = p >= 2 ? t : t - 1;
+      // the update of this step's parameter lands during this step (P <= 2): priors
+      // after the barrier
+      const bool post_prior = P == 1 ? aux_now : (P == 2 && comp_now);
       // proposal (Parameter.propose :304-306): value + (proposalSd=1 * scale) * z
       const double v = th[p * 64];
       const double s = st[(NMC_ST_S * P + p) * 64];
       const double zc = lds[(L.zl + 2 * sp) * 64 + 2 * lane];
       const double prop = v + (1.0 * s) * zc;
+      // this step's priors (:293-294) from the hyper-parameters in LDS -- by the wave that
+      // has just updated them when that update lands during this step (post_prior)
+      auto step_priors = [&]() {
+        const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
+        const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
+        cwv[NMC_CW_LPC * 64] =
+            t > 0 ? nmc_norm_logpdf_r(v, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
+        cwv[NMC_CW_LPP * 64] = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
+      };
       // ---- control wave, before the barrier: next variates in flight, priors, and both
       //      outcomes of the decision -- accept (sA, naA, nrA, ta + 1) / reject (sR,
       //      naR, nrR, ta), tuned if due -- parked in LDS (no registers live across
       //      the likelihood region) ----
-      double* cwv = lds + L.cw * 64 + lane;    // cwv[k * 64]
       if (ctl) {
+        if (pend_p >= 0) apply_pending();
         if constexpr (sync) {   // the previous step's value is stored; count it published
           if (pub_p >= 0) {
             nmc_drain_vm();
@@ -784,8 +842,8 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         const int pn = p + 1 < P ? p + 1 : 0;
         if (tn < i1) nmc_dma16(zl_src(tn, pn), lds + (L.zl + 2 * (sp ^ 1)) * 64);
         if (!hl && hyper_now) nmc_hyper_variates(d, cb, t - 1, lds, L, 0, 1);
-        if (PARTIAL && p == (P > 1 ? 1 : 0)) nmc_hyper_sdm(d, lds, L, lane);
-        if (!hyper_now && !(hl && P == 1 && aux_now)) {   // priors (:293-294)
+        if (PARTIAL && !hl && p == (P > 1 ? 1 : 0)) nmc_hyper_sdm(d, lds, L, lane);
+        if (!hyper_now && !(hl && post_prior)) {   // priors (:293-294)
           double lpc, lpp;
           if (PARTIAL) {
             const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
@@ -800,63 +858,76 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
           cwv[NMC_CW_LPP * 64] = lpp;
         }
       }
-      // ---- auxiliary waves 1..NAUX: the Gibbs update of parameter aq after iteration
-      //      atq, overlapped with this step's likelihood: wave 1 waits for the chain
-      //      block's counter of aq, each copies 1/NAUX of the groups' values into LDS
-      //      (one batch of sc1 loads), they join through LDS epoch words, wave 1
-      //      updates the hyper-parameters ----
-      const bool aux = aux_now && w >= 1 && w <= naux;
+      // ---- auxiliary waves, overlapped with this step's likelihood: loader wave 1 waits
+      //      for the chain block's counter of task gs-1, each loader copies its share of
+      //      the groups' values into LDS (one batch of sc1 loads); P == 1: they join
+      //      through LDS epoch words and wave 1 computes; P >= 2: the compute wave (the
+      //      last auxiliary) updates task gs-2 from the buffer the loaders filled at the
+      //      previous step ----
+      const int nload = pipe ? naux - 1 : naux;
+      const bool aux = hl && w >= 1 && w <= naux && (w <= nload ? aux_now : comp_now);
       if constexpr (hl) if (aux) {
         const int a = w - 1;
-        double hz = 0.0, hx = 0.0;
-        if (a == 0) {   // this lane's hyper variates of (atq, aq), issued early
-          const size_t hvi = (((size_t)(atq - d.vbase) * P + aq) * C + cc) * 2;
-          hz = d.vh[hvi];
-          hx = d.vh[hvi + 1];
-        }
-        const double want = 2.0 * ((double)t * P + p + 1);      // this step's epoch
-        double* flagw = lds + L.flag * 64 + 1;
-        if (a == 0 && lane == 0)
-          __hip_atomic_store(flagw,
-                             nmc_poll_published(d, cb, aq, (unsigned)G * (unsigned)(atq - i0 + 1))
-                                 ? want : -want,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        double f;
-        while (true) {
-          f = __hip_atomic_load(flagw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (f == want || f == -want) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        // keep the payload loads below the poll (no instruction: wavefront scope)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (p == 0) NMC_STAMP_AUX(t, 13);
-        if (f == want) {
-          const double* src = (atq & 1) ? d.vb1 : d.vb0;
-          nmc_hyper_load(d, src, aq, cc, (int)(((int64_t)G * a) / naux),
-                         (int)(((int64_t)G * (a + 1)) / naux), lds, L);
-          if (p == 0) NMC_STAMP_AUX(t, 14);
-          // join: each auxiliary wave stamps its LDS word with the epoch once its share
-          // has landed; wave 1 waits for all of them (bounded)
-          double* joinw = lds + L.flag * 64 + 8;
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if (lane == 0) __hip_atomic_store(joinw + a, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (a == 0) {
-            for (int k = 1; k < naux; ++k)
-              for (unsigned spins = 0;
-                   __hip_atomic_load(joinw + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != want &&
-                   spins < NMC_SPIN_LIMIT;
-                   ++spins)
-                __builtin_amdgcn_s_sleep(1);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (p == 0) NMC_STAMP_AUX(t, 15);
-            nmc_hyper_compute(d, cb, atq, aq, lds, L, g == 0, hz, hx);
-            if (p == 0) NMC_STAMP_AUX(t, 12);
+        if (a < nload) {
+          double hz = 0.0, hx = 0.0;
+          if (!pipe && a == 0) {   // this lane's hyper variates of (atq, aq), issued early
+            const size_t hvi = (((size_t)(atq - d.vbase) * P + aq) * C + cc) * 2;
+            hz = d.vh[hvi];
+            hx = d.vh[hvi + 1];
           }
+          const double want = 2.0 * ((double)gs + 1);      // this step's epoch
+          double* flagw = lds + L.flag * 64 + 1;
+          if (a == 0 && lane == 0)
+            __hip_atomic_store(flagw,
+                               nmc_poll_published(d, cb, aq, (unsigned)G * (unsigned)(atq - i0 + 1))
+                                   ? want : -want,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          double f;
+          while (true) {
+            f = __hip_atomic_load(flagw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (f == want || f == -want) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          // keep the payload loads below the poll (no instruction: wavefront scope)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if (p == 0) NMC_STAMP_AUX(t, 13);
+          if (f == want) {
+            const double* src = (atq & 1) ? d.vb1 : d.vb0;
+            nmc_hyper_load(d, src, aq, cc, (int)(((int64_t)G * a) / nload),
+                           (int)(((int64_t)G * (a + 1)) / nload), lds, L, ((gs - 1) & 1) * G);
+            if (p == 0) NMC_STAMP_AUX(t, 14);
+            if (!pipe) {
+              // join: each loader stamps its LDS word with the epoch once its share has
+              // landed; wave 1 waits for all of them (bounded)
+              double* joinw = lds + L.flag * 64 + 8;
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+              if (lane == 0)
+                __hip_atomic_store(joinw + a, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              if (a == 0) {
+                for (int k = 1; k < nload; ++k)
+                  for (unsigned spins = 0;
+                       __hip_atomic_load(joinw + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) !=
+                           want &&
+                       spins < NMC_SPIN_LIMIT;
+                       ++spins)
+                    __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (p == 0) NMC_STAMP_AUX(t, 15);
+                nmc_hyper_compute(d, cb, atq, aq, lds, L, g == 0, hz, hx, ((gs - 1) & 1) * G);
+                if (post_prior) step_priors();
+                if (p == 0) NMC_STAMP_AUX(t, 12);
+              }
+            }
+          }
+        } else {   // compute wave: task gs-2, loaded into buffer (gs-2)&1 at step gs-1
+          const size_t hvi = (((size_t)(ctq - d.vbase) * P + cq) * C + cc) * 2;
+          nmc_hyper_compute(d, cb, ctq, cq, lds, L, g == 0, d.vh[hvi], d.vh[hvi + 1],
+                            (gs & 1) * G);
+          if (post_prior) step_priors();
+          if (p == 0) NMC_STAMP_AUX(t, 12);
         }
       }
       // ---- likelihood of the proposal over this wave's rows (:615-635) ----
-      const int l0 = W == 1 ? 0 : 1 + naux;
-      const int nll = W - l0;
       if (w >= l0 && !aux) {
         const int k = w - l0;
         int64_t ra;
@@ -872,7 +943,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         else              // wave-uniform global address: scalar loads
           nmc_ll_rows(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, acc);
 #pragma unroll
-        for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * W + k) * 64 + lane] = acc[j];
+        for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * 16 + k) * 64 + lane] = acc[j];
       }
       NMC_STAMP(t, 1 + 3 * (p & 1));
       if (ctl) nmc_drain_vm();   // this wave's LDS-DMA has landed
@@ -880,14 +951,10 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       NMC_STAMP(t, 2 + 3 * (p & 1));
 
       // ---- Gibbs update after iteration t-1 (needed by this iteration's priors) ----
-      if constexpr (hl) if (aux_now) {   // the auxiliary waves' verdict
-        ok = lds[L.flag * 64 + 1] == 2.0 * ((double)t * P + p + 1);
-        if (!ok) break;
-        if (P == 1 && ctl) {   // the update just made is this step's prior
-          const double m = hy[NMC_HY_MU * 64], sd = hy[NMC_HY_SD * 64];
-          const double lsd = hy[NMC_HY_LSD * 64], isd = hy[NMC_HY_ISD * 64];
-          cwv[NMC_CW_LPC * 64] = nmc_norm_logpdf_r(cwv[NMC_CW_V * 64], m, sd, isd, lsd);
-          cwv[NMC_CW_LPP * 64] = nmc_norm_logpdf_r(cwv[NMC_CW_PROP * 64], m, sd, isd, lsd);
+      if constexpr (hl) {
+        if (aux_now) {   // the loaders' verdict
+          ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
+          if (!ok) break;
         }
       }
       if constexpr (PARTIAL && !hl) if (hyper_now) {
@@ -912,19 +979,19 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       //      the Metropolis decision, one chain per lane (:334-383) ----
       if (ctl) {
         double acc[Fam::NACC];
-        const int nll_s = W == 1 ? 1 : W - 1 - naux;
 #pragma unroll
         for (int j = 0; j < Fam::NACC; ++j) {
           // the likelihood waves' partials in a fixed order: wave k into accumulator
-          // k % 4, combined (a0+a1)+(a2+a3); every LDS read in flight at once
-          const double* pt = lds + (L.part + j * W) * 64 + lane;
+          // k % 4, combined (a0+a1)+(a2+a3); every LDS read in flight at once (slots
+          // past the last likelihood wave hold -0.0)
+          const double* pt = lds + (L.part + j * 16) * 64 + lane;
           double a4[4] = {0.0, 0.0, 0.0, 0.0};
           double v16[16];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) v16[u] = u < nll_s ? pt[u * 64] : 0.0;
+          for (int u = 0; u < 16; ++u) v16[u] = pt[u * 64];
 #pragma unroll
           for (int u = 0; u < 16; ++u)
-            if (u < nll_s) a4[u & 3] = u < 4 ? v16[u] : a4[u & 3] + v16[u];
+            a4[u & 3] = u < 4 ? v16[u] : a4[u & 3] + v16[u];
           acc[j] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
         }
         if (p == 0) NMC_STAMP(t, 10);
@@ -955,23 +1022,15 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
           pub_p = p;
         }
         st[(NMC_ST_S * P + p) * 64] = cwv[(accept ? NMC_CW_SA : NMC_CW_SR) * 64];
-        st[(NMC_ST_LP * P + p) * 64] = accept ? lpp : lpc;
-        st[(NMC_ST_NA * P + p) * 64] = cwv[(accept ? NMC_CW_NAA : NMC_CW_NAR) * 64];
-        st[(NMC_ST_NR * P + p) * 64] = cwv[(accept ? NMC_CW_NRA : NMC_CW_NRR) * 64];
-        st[(NMC_ST_TA * P + p) * 64] = cwv[NMC_CW_TA * 64] + (accept ? 1.0 : 0.0);
-        if (accept) LL = llp;
+        cwv[NMC_CW_PAC * 64] = accept ? 1.0 : 0.0;
+        cwv[NMC_CW_PLP * 64] = accept ? lpp : lpc;
+        cwv[NMC_CW_PLL * 64] = llp;
+        pend_p = p;
+        pend_t = t;
+        // no pooling: the rest waits for the next step's pre-barrier slack; partial pooling:
+        // at once (measured faster: the next step's slack feeds the Gibbs hand-off)
+        if (PARTIAL) apply_pending();
         if (p == 0) NMC_STAMP(t, 12);
-        if (live) {
-          if (row_rec >= 0) {
-            const int col = p * (G + (PARTIAL ? 2 : 0)) + (PARTIAL ? 2 : 0) + g;
-            d.samples[((size_t)row_rec * d.cols + col) * C + c] = vn;
-          }
-          if (t < d.trace_n) {
-            const size_t it = (((size_t)t * P + p) * G + g) * C + c;
-            d.tflag[it] = accept ? 1 : 0;
-            d.tllp[it] = llp;
-          }
-        }
       }
       if (p == 0) NMC_STAMP(t, 3);
       __syncthreads();      // the new value is visible to every wave
@@ -988,6 +1047,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
                              __HIP_MEMORY_SCOPE_AGENT);
   }
 
+  if (ctl && pend_p >= 0) apply_pending();
   // ---- epilogue: state back to HBM (control wave) ----
   if (ctl && live && ok) {
     double* vo = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
@@ -1003,15 +1063,25 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     d.ll[gc] = LL;
   }
   // ---- closing Gibbs update after i1-1 (group-0 workgroups write and record it) ----
-  if constexpr (hl) if (ok && g == 0) {   // only the last parameter is left
+  if constexpr (hl) if (ok && g == 0) {
+    const int ge = i1 * P;   // tasks ge-2 (loaded at the last step; P >= 2) and ge-1 are left
+    const bool pipe = P >= 2;
+    const int nload = pipe ? naux - 1 : naux;
+    if (pipe && w == naux) {
+      const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 2)) * C + cc) * 2;
+      nmc_hyper_compute(d, cb, i1 - 1, P - 2, lds, L, true, d.vh[hvi], d.vh[hvi + 1],
+                        ((ge - 2) & 1) * G);
+    }
     if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L)) {
-      if (w >= 1 && w <= naux)
+      if (w >= 1 && w <= nload)
         nmc_hyper_load(d, ((i1 - 1) & 1) ? d.vb1 : d.vb0, P - 1, cc,
-                       (int)(((int64_t)G * (w - 1)) / naux), (int)(((int64_t)G * w) / naux), lds, L);
+                       (int)(((int64_t)G * (w - 1)) / nload), (int)(((int64_t)G * w) / nload), lds,
+                       L, ((ge - 1) & 1) * G);
       __syncthreads();
       if (w == 1) {
         const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 1)) * C + cc) * 2;
-        nmc_hyper_compute(d, cb, i1 - 1, P - 1, lds, L, true, d.vh[hvi], d.vh[hvi + 1]);
+        nmc_hyper_compute(d, cb, i1 - 1, P - 1, lds, L, true, d.vh[hvi], d.vh[hvi + 1],
+                          ((ge - 1) & 1) * G);
       }
     }
   }

@@ -56,6 +56,7 @@ struct nmc_ctx {
   double step_ms = 0, hyper_ms = 0;
   long long step_n = 0, hyper_n = 0;
   long long step_iters = 0;
+  int launch_iters = 0;                    // cap on iterations per launch (0: vcap)
   std::vector<int> kev_iters;             // iterations covered by each timed step launch
   int cur_slot = 1;                       // values after the last iteration: vb[cur_slot]
   int nacc = 1;                           // likelihood accumulators of the family
@@ -162,12 +163,13 @@ static void choose_geometry(nmc_ctx* x) {
     if (v >= 1 && v <= 16) w = v;
   }
   d.W = (int)w;
-  // partial pooling: NAUX = ceil(G / 32) (<= 4) auxiliary waves, one batch of 32
-  // loads each per Gibbs update; reserved in every partial mode so the likelihood
+  // partial pooling: NAUX = ceil(G / 32) (<= 4) loader waves, one batch of 32 loads
+  // each per Gibbs update; reserved in every partial mode so the likelihood
   // partition (W - 1 - NAUX waves) is the same whatever the launch mode
   d.naux = 0;
   if (x->pooling == NMC_POOL_PARTIAL) {
-    const int na = (d.G + 31) / 32 < 4 ? (d.G + 31) / 32 : 4;
+    // (+1 compute wave when P >= 2: the update is pipelined over two steps)
+    const int na = ((d.G + 31) / 32 < 4 ? (d.G + 31) / 32 : 4) + (d.P >= 2 ? 1 : 0);
     if (d.W >= na + 2 && d.G <= 128) d.naux = na;
   }
   // rows in LDS when they fit beside the rest of the carve (64 KiB for the rows)
@@ -176,6 +178,7 @@ static void choose_geometry(nmc_ctx* x) {
                !(getenv("NMC_NO_LDS_ROWS") && atoi(getenv("NMC_NO_LDS_ROWS")));
   // the persistent Gibbs update by the auxiliary waves needs G <= 128 (one numpy
   // leaf) and one parameter's chain-block values in LDS
+  d.noprio = getenv("NMC_NOPRIO") && atoi(getenv("NMC_NOPRIO"));
   d.hlds = d.naux > 0 && d.G <= 128 && lds_bytes_for(x, 1, d.rows_lds) <= (size_t)160 * 1024 &&
            !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
 }
@@ -594,8 +597,10 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
     x->cur_slot = need;
   }
   int rc = with_family(x, [&](auto fam) -> int {
-    for (int c0 = iter_begin; c0 < iter_end; c0 += x->d.vcap) {
-      const int c1 = c0 + x->d.vcap < iter_end ? c0 + x->d.vcap : iter_end;
+    const int chunk =
+        x->launch_iters > 0 && x->launch_iters < x->d.vcap ? x->launch_iters : x->d.vcap;
+    for (int c0 = iter_begin; c0 < iter_end; c0 += chunk) {
+      const int c1 = c0 + chunk < iter_end ? c0 + chunk : iter_end;
       // every variate of iterations [c0, c1) in one fully parallel launch
       x->d.vbase = c0;
       const size_t n = (size_t)(c1 - c0) * P * x->C * (x->G + (partial ? 1 : 0));
@@ -705,6 +710,12 @@ int nmc_event_elapsed(nmc_ctx* x, int a, int b, float* ms) {
   hipSetDevice(x->device);
   HIPCHK(hipEventSynchronize(x->ev[b]));
   HIPCHK(hipEventElapsedTime(ms, x->ev[a], x->ev[b]));
+  return 0;
+}
+
+int nmc_set_launch_iters(nmc_ctx* x, int max_iters) {
+  if (max_iters < 0) return fail(-1, "max_iters < 0");
+  x->launch_iters = max_iters;
   return 0;
 }
 

@@ -59,6 +59,7 @@ SIGNATURES = {
     "nmc_event_elapsed": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_float)]),
     "nmc_set_kernel_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "nmc_set_launch_iters": (ctypes.c_int, [_vp, ctypes.c_int]),
     "nmc_get_kernel_timing": (ctypes.c_int, [_vp, _c_double_p, _c_int64_p, _c_int64_p,
                                              _c_double_p, _c_int64_p]),
     "nmc_launch_config": (ctypes.c_int, [_vp, _c_int_p, _c_int_p, _c_int_p]),

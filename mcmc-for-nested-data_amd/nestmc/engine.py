@@ -174,6 +174,10 @@ class Engine:
         check(self.lib.nmc_event_elapsed(self.h, a, b, ctypes.byref(ms)))
         return ms.value
 
+    def set_launch_iters(self, n):
+        """Cap the iterations one persistent launch covers (0: the variate chunk)."""
+        check(self.lib.nmc_set_launch_iters(self.h, int(n)))
+
     def set_kernel_timing(self, enable):
         check(self.lib.nmc_set_kernel_timing(self.h, 1 if enable else 0))
 
