@@ -58,7 +58,7 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
                      priorDistribution=None, startWithMLE=False, startingPointValueRange=None,
                      nProcesses=1, displayProgress=True, loggingLevel="info", *,
                      seed=0, devices=None, rng="philox", chains=None, return_samples=False,
-                     write_files=True):
+                     write_files=True, replay=None):
     """Drop-in for posteriorSampling.samplePosterior (same positional/keyword API).
 
     Extra keyword-only options (all optional):
@@ -66,6 +66,8 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
       devices    GPU ids to shard chains over (default: [0]); chains are split in
                  contiguous blocks so chain c always draws the same stream
       rng        "philox" (default) or "replay" (test use)
+      replay     rng="replay": dict of captured variates z, u [C, iter, P, G] and
+                 hz, hu [C, iter, P] (chain axis = position in ``chains``)
       chains     run only these global chain ids (multi-process sharding)
       return_samples  also return {"rows": [C][rows][cols], "row_index", "header"}
     nProcesses sizes the host threads used for chain initialisation and CSV writing.
@@ -109,11 +111,16 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
         priors = list(priorDistribution)
     elif priorDistribution is not None and logger:
         logger.info("Partial pooling ignores prior distribution.")
+    # partial pooling still draws start values from the priors when given
+    # (MCMC._findStartingPoint :1076-1077); the sampler itself ignores them (:713-715)
+    start_priors = list(priorDistribution) if priorDistribution is not None else None
     if pooling == "partial" and G < 2:
         raise ValueError("partial pooling needs at least two groups (the invgamma update of "
                          "posteriorSampling.py:494-498 has shape (G-1)/2)")
 
     chain_ids = list(range(nChains)) if chains is None else [int(c) for c in chains]
+    if (rng == "replay") != (replay is not None):
+        raise ValueError("rng='replay' needs replay= variates (and only then)")
     if _lib.device_count() < 1:
         raise _lib.NestmcError("no HIP device visible: the sampler runs on MI355X only")
     devices = [0] if devices is None else list(devices)
@@ -129,7 +136,7 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
                                    loggingLevel)
             lg.info("chain %i. Started looking for a reasonable starting state." % c)
             chain_logs.append(lg)
-    st = init_chains(logLikelihoodFunction, sizes, names, chain_ids, pooling, priors,
+    st = init_chains(logLikelihoodFunction, sizes, names, chain_ids, pooling, start_priors,
                      startingPointValueRange, startWithMLE, threads=threads)
 
     # ---- shard contiguous blocks of chains over the devices -----------------
@@ -147,6 +154,8 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
         eng.set_state(st["value"][sl], st["log_prior"][sl], st["ll"][sl],
                       None if st["mu"] is None else st["mu"][sl],
                       None if st["s2"] is None else st["s2"][sl])
+        if replay is not None:
+            eng.set_replay(*(numpy.asarray(replay[k])[sl] for k in ("z", "u", "hz", "hu")))
         eng.set_schedule(nIter, burn, thin, 100)
         engines.append((eng, s0, ids))
 

@@ -1,0 +1,33 @@
+"""The drop-in API end to end on the GPU: sample_posterior (the rebuild's
+samplePosterior, posteriorSampling.py:28-35) run with the reference's own variates
+(replayed) must write sample.<chain>.csv files byte-identical to the ones the
+reference wrote for the same inputs (tests/golden/csv, captured by
+tests/golden/make_golden.py) -- host init (RandomState(chain) order), the device
+loop, the schedule/recorder and the "%f" CSV writer together.
+"""
+
+import filecmp
+import os
+
+import pytest
+
+from golden_cases import CASES, Case
+from gpu_cases import family_for
+from nestmc.sampler import sample_posterior
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_sample_posterior_writes_reference_csvs(gpu_lib, name, tmp_path):
+    c = Case(name)
+    a = c.arr
+    out = str(tmp_path) + "/"
+    sample_posterior(c.n_chains, c.n_iter, c.n_samples, c.names, c.n_groups, c.n_per_group,
+                     c.pooling, family_for(c), out, saveLogLikelihood=False,
+                     priorDistribution=c.priors, startWithMLE=c.mle,
+                     startingPointValueRange=c.ranges, displayProgress=False,
+                     rng="replay", replay={k: a[k] for k in ("z", "u", "hz", "hu")})
+    for ch in range(c.n_chains):
+        mine = os.path.join(out, "sample", "sample.%i.csv" % ch)
+        assert filecmp.cmp(mine, c.csv_path(ch), shallow=False), (name, ch)
