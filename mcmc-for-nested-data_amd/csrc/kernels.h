@@ -207,15 +207,15 @@ __global__ void __launch_bounds__(256) nmc_k_fill(Dev d, int iter0, int T) {
 // ---------------------------------------------------------------------------
 struct nmc_lds_layout {
   int th;      // [P]            current values (control wave writes, all read)
-  int part;    // [NACC][W]      per-wave likelihood partial sums
+  int part;    // [NACC][16]     per-wave likelihood partial sums (unused slots: -0.0)
   int st;      // [5][P]         scale, log prior, n acc, n rej, total acc (control wave)
   int hyp;     // [6][P]         mu, sd, log sd, sigma2, sqrt(sigma2/G), 1/sd of the hyper-prior
-  int hval;    // [G]            Gibbs payload of one parameter (payload-in-LDS mode)
+  int hval;    // [2][G]         Gibbs payload of one task, two buffers (payload-in-LDS mode)
   int hst;     // [P][nleaf][8 + ntail]  stream sums / tail elements (pairwise sum)
   int hleaf;   // [P][nleaf]     leaf sums
   int zl;      // [2][2]         {z, log u} of this and the next step (LDS-DMA, step parity)
   int hv;      // [2P]           {hyper z, gamma} of the Gibbs update (LDS-DMA)
-  int cw;      // [12]           control-wave temporaries across the step barrier
+  int cw;      // [15]           control-wave temporaries across the step barrier
   int flag;    // [1]            broadcast word
   int rows;    // [nrows_lds][NF] the group's observation rows (staged once per launch)
   int total;   // columns

@@ -1,7 +1,9 @@
 """nestmc: MI355X-native engine for the MCMC inner loop of MCMC-for-Nested-Data.
 
-Public entry points mirror the reference (posteriorSampling.samplePosterior,
-sampleDiagnosis.diagnoseSamples; see the drop-in modules next to this package).
+The public entry point mirrors the reference's posteriorSampling.samplePosterior
+(drop-in module next to this package).  The sample files it writes are
+byte-identical to the reference's, so the reference's
+sampleDiagnosis.diagnoseSamples reads them unchanged.
 """
 
 from .data import example_distribution, example_regression, linreg, logistic  # noqa: F401

@@ -105,6 +105,7 @@ def main():
     cases += [("linreg", 256, 64, 1000, "none", w) for w in (0, 8)]
     if not a.quick:
         cases += [("linreg", 1024, 256, 2000, "partial", 0),
+                  ("linreg", 128, 256, 2000, "partial", 0),      # cfg 4, one rank of 8
                   ("gauss", 256, 32, 500, "none", 0),
                   ("logistic", 64, 128, 5000, "partial", 0)]
     for c in cases:
