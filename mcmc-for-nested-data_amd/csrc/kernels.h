@@ -210,7 +210,7 @@ struct nmc_lds_layout {
   int part;    // [NACC][16]     per-wave likelihood partial sums (unused slots: -0.0)
   int st;      // [5][P]         scale, log prior, n acc, n rej, total acc (control wave)
   int hyp;     // [6][P]         mu, sd, log sd, sigma2, sqrt(sigma2/G), 1/sd of the hyper-prior
-  int hval;    // [2][G]         Gibbs payload of one task, two buffers (payload-in-LDS mode)
+  int hval;    // [2][G + 1]     Gibbs payload of one task, two buffers (payload-in-LDS mode)
   int hst;     // [P][nleaf][8 + ntail]  stream sums / tail elements (pairwise sum)
   int hleaf;   // [P][nleaf]     leaf sums
   int zl;      // [2][2]         {z, log u} of this and the next step (LDS-DMA, step parity)
@@ -229,7 +229,7 @@ __host__ __device__ inline nmc_lds_layout nmc_lds(int nacc, int P, int partial, 
   L.st = L.part + nacc * 16;   // 16 partial slots per accumulator (unused: -0.0)
   L.hyp = L.st + 5 * P;
   L.hval = L.hyp + (partial ? 6 * P : 0);
-  L.hst = L.hval + (partial && hlds ? 2 * G : 0);   // two task buffers
+  L.hst = L.hval + (partial && hlds ? 2 * (G + 1) : 0);   // two task buffers, each + 1 DMA pad
   L.hleaf = L.hst + (partial ? P * nleaf * (8 + ntail) : 0);
   L.zl = L.hleaf + (partial ? P * nleaf : 0);
   L.hv = L.zl + 4;
@@ -463,21 +463,40 @@ __device__ __forceinline__ double nmc_leaf_sum(const double* v, int n, double mu
 }
 
 // Groups [kb, ke) of the chain block's published values of parameter p (64 chains
-// each) -> LDS hval, sc1 loads, 32 in flight.
+// each) -> LDS hval, sc1 loads, 8 in flight (used when C is odd).
 __device__ __forceinline__ void nmc_hyper_load(const Dev& d, const double* src, int p, int cc,
                                                int kb, int ke, double* lds,
                                                const nmc_lds_layout& L, int hoff) {
   const int lane = threadIdx.x & 63;
   const int C = d.C;
   src += (size_t)p * d.G * C;
-  for (int k0 = kb; k0 < ke; k0 += 32) {
-    double tv[32];
+  constexpr int NB = 8;   // the odd-C fallback of the LDS-DMA copy: few registers
+  for (int k0 = kb; k0 < ke; k0 += NB) {
+    double tv[NB];
 #pragma unroll
-    for (int u = 0; u < 32; ++u)
+    for (int u = 0; u < NB; ++u)
       tv[u] = k0 + u < ke ? nmc_ldv<NMC_SRC_SC1>(src + (size_t)(k0 + u) * C + cc) : 0.0;
 #pragma unroll
-    for (int u = 0; u < 32; ++u)
+    for (int u = 0; u < NB; ++u)
       if (k0 + u < ke) lds[(size_t)(L.hval + hoff + k0 + u) * 64 + lane] = tv[u];
+  }
+}
+
+// The same by LDS-DMA (global_load_lds_dwordx4, sc1): one instruction moves two groups'
+// 64-chain rows (lanes 0-31 / 32-63, two chains per lane) into two consecutive hval
+// columns, so one wave has the whole payload in flight without registers.  Needs C
+// even (16-byte rows); an odd group count writes one pad column past ke.  The issuing
+// wave retires the copies with s_waitcnt vmcnt(0).
+__device__ __forceinline__ void nmc_hyper_dma(const Dev& d, const double* src, int p, int cb,
+                                              int kb, int ke, double* lds,
+                                              const nmc_lds_layout& L, int hoff) {
+  const int lane = threadIdx.x & 63;
+  const double* s = src + (size_t)p * d.G * d.C + (size_t)cb * 64 + 2 * (lane & 31);
+  for (int k0 = kb; k0 < ke; k0 += 2) {
+    const int gk = k0 + (lane >> 5) < ke ? k0 + (lane >> 5) : ke - 1;
+    __builtin_amdgcn_global_load_lds((nmc_glb_ptr)(s + (size_t)gk * d.C),
+                                     (nmc_lds_ptr)(lds + (size_t)(L.hval + hoff + k0) * 64), 16,
+                                     0, 16 /* sc1 */);
   }
 }
 
@@ -521,12 +540,24 @@ __device__ __forceinline__ void nmc_hyper_compute(const Dev& d, int cb, int t, i
   }
 }
 
-// Thread 0 of the calling wave polls the chain block's publish counter until it
-// reaches target (bounded; a timeout is recorded in d.tmo and reported by the host).
+// The calling wave polls the chain block's publish counter until it reaches target
+// (bounded; a timeout is recorded in d.tmo and reported by the host).  The counter is
+// sharded 8 ways (workgroup g adds to shard g % 8, each shard on its own 128-B line)
+// so the G arrivals do not serialise on one line; lanes 0-7 read the shards with one
+// sc1 load and the wave sums them.  Wave-uniform result; call with the whole wave.
+__device__ __forceinline__ unsigned* nmc_counter(const Dev& d, int cb, int p, int shard) {
+  return d.cnt + (((size_t)cb * d.P + p) * 8 + shard) * 32;
+}
 __device__ __forceinline__ bool nmc_poll_published(const Dev& d, int cb, int p, unsigned target) {
-  unsigned* ctr = d.cnt + ((size_t)cb * d.P + p) * 32;
+  const int lane = threadIdx.x & 63;
+  unsigned* ctr = nmc_counter(d, cb, p, lane & 7);
   for (unsigned spins = 0;; ++spins) {
-    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+    const unsigned v =
+        lane < 8 ? __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    unsigned tot = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tot += __builtin_amdgcn_readlane(v, k);
+    if (tot >= target) return true;
     if ((spins & 255) == 255 &&
         __hip_atomic_load(d.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
       return false;
@@ -541,7 +572,10 @@ __device__ __forceinline__ bool nmc_poll_published(const Dev& d, int cb, int p, 
 // Whole-workgroup wait (thread 0 polls, result broadcast through LDS).
 __device__ __forceinline__ bool nmc_wait_published(const Dev& d, int cb, int p, unsigned target,
                                                    double* lds, const nmc_lds_layout& L) {
-  if (threadIdx.x == 0) lds[L.flag * 64] = nmc_poll_published(d, cb, p, target) ? 1.0 : 0.0;
+  if (threadIdx.x < 64) {
+    const bool r = nmc_poll_published(d, cb, p, target);
+    if (threadIdx.x == 0) lds[L.flag * 64] = r ? 1.0 : 0.0;
+  }
   __syncthreads();
   // keep the payload loads below the poll (no instruction: wavefront scope)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -815,7 +849,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
           if (pub_p >= 0) {
             nmc_drain_vm();
             if (lane == 0)
-              __hip_atomic_fetch_add(d.cnt + ((size_t)cb * P + pub_p) * 32, 1u, __ATOMIC_RELAXED,
+              __hip_atomic_fetch_add(nmc_counter(d, cb, pub_p, g & 7), 1u, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
             pub_p = -1;
           }
@@ -877,11 +911,12 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
           }
           const double want = 2.0 * ((double)gs + 1);      // this step's epoch
           double* flagw = lds + L.flag * 64 + 1;
-          if (a == 0 && lane == 0)
-            __hip_atomic_store(flagw,
-                               nmc_poll_published(d, cb, aq, (unsigned)G * (unsigned)(atq - i0 + 1))
-                                   ? want : -want,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (a == 0) {
+            const bool r = nmc_poll_published(d, cb, aq, (unsigned)G * (unsigned)(atq - i0 + 1));
+            if (lane == 0)
+              __hip_atomic_store(flagw, r ? want : -want, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
           double f;
           while (true) {
             f = __hip_atomic_load(flagw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -893,8 +928,13 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
           if (p == 0) NMC_STAMP_AUX(t, 13);
           if (f == want) {
             const double* src = (atq & 1) ? d.vb1 : d.vb0;
-            nmc_hyper_load(d, src, aq, cc, (int)(((int64_t)G * a) / nload),
-                           (int)(((int64_t)G * (a + 1)) / nload), lds, L, ((gs - 1) & 1) * G);
+            if (nload == 1 && (C & 1) == 0) {
+              nmc_hyper_dma(d, src, aq, cb, 0, G, lds, L, ((gs - 1) & 1) * (G + 1));
+              nmc_drain_vm();
+            } else {
+              nmc_hyper_load(d, src, aq, cc, (int)(((int64_t)G * a) / nload),
+                             (int)(((int64_t)G * (a + 1)) / nload), lds, L, ((gs - 1) & 1) * (G + 1));
+            }
             if (p == 0) NMC_STAMP_AUX(t, 14);
             if (!pipe) {
               // join: each loader stamps its LDS word with the epoch once its share has
@@ -913,7 +953,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
                     __builtin_amdgcn_s_sleep(1);
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 if (p == 0) NMC_STAMP_AUX(t, 15);
-                nmc_hyper_compute(d, cb, atq, aq, lds, L, g == 0, hz, hx, ((gs - 1) & 1) * G);
+                nmc_hyper_compute(d, cb, atq, aq, lds, L, g == 0, hz, hx, ((gs - 1) & 1) * (G + 1));
                 if (post_prior) step_priors();
                 if (p == 0) NMC_STAMP_AUX(t, 12);
               }
@@ -922,7 +962,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         } else {   // compute wave: task gs-2, loaded into buffer (gs-2)&1 at step gs-1
           const size_t hvi = (((size_t)(ctq - d.vbase) * P + cq) * C + cc) * 2;
           nmc_hyper_compute(d, cb, ctq, cq, lds, L, g == 0, d.vh[hvi], d.vh[hvi + 1],
-                            (gs & 1) * G);
+                            (gs & 1) * (G + 1));
           if (post_prior) step_priors();
           if (p == 0) NMC_STAMP_AUX(t, 12);
         }
@@ -1043,7 +1083,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   if constexpr (sync) if (ctl && pub_p >= 0) {   // the last parameter's count
     nmc_drain_vm();
     if (lane == 0)
-      __hip_atomic_fetch_add(d.cnt + ((size_t)cb * P + pub_p) * 32, 1u, __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add(nmc_counter(d, cb, pub_p, g & 7), 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
   }
 
@@ -1070,18 +1110,24 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     if (pipe && w == naux) {
       const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 2)) * C + cc) * 2;
       nmc_hyper_compute(d, cb, i1 - 1, P - 2, lds, L, true, d.vh[hvi], d.vh[hvi + 1],
-                        ((ge - 2) & 1) * G);
+                        ((ge - 2) & 1) * (G + 1));
     }
     if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L)) {
-      if (w >= 1 && w <= nload)
-        nmc_hyper_load(d, ((i1 - 1) & 1) ? d.vb1 : d.vb0, P - 1, cc,
-                       (int)(((int64_t)G * (w - 1)) / nload), (int)(((int64_t)G * w) / nload), lds,
-                       L, ((ge - 1) & 1) * G);
+      if (w >= 1 && w <= nload) {
+        const double* src = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
+        if (nload == 1 && (C & 1) == 0) {
+          nmc_hyper_dma(d, src, P - 1, cb, 0, G, lds, L, ((ge - 1) & 1) * (G + 1));
+          nmc_drain_vm();
+        } else {
+          nmc_hyper_load(d, src, P - 1, cc, (int)(((int64_t)G * (w - 1)) / nload),
+                         (int)(((int64_t)G * w) / nload), lds, L, ((ge - 1) & 1) * (G + 1));
+        }
+      }
       __syncthreads();
       if (w == 1) {
         const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 1)) * C + cc) * 2;
         nmc_hyper_compute(d, cb, i1 - 1, P - 1, lds, L, true, d.vh[hvi], d.vh[hvi + 1],
-                          ((ge - 1) & 1) * G);
+                          ((ge - 1) & 1) * (G + 1));
       }
     }
   }

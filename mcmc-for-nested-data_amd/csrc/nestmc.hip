@@ -163,13 +163,14 @@ static void choose_geometry(nmc_ctx* x) {
     if (v >= 1 && v <= 16) w = v;
   }
   d.W = (int)w;
-  // partial pooling: NAUX = ceil(G / 32) (<= 4) loader waves, one batch of 32 loads
-  // each per Gibbs update; reserved in every partial mode so the likelihood
+  // partial pooling: one loader wave (the payload is LDS-DMA, no registers) + one
+  // compute wave when P >= 2; reserved in every partial mode so the likelihood
   // partition (W - 1 - NAUX waves) is the same whatever the launch mode
   d.naux = 0;
   if (x->pooling == NMC_POOL_PARTIAL) {
-    // (+1 compute wave when P >= 2: the update is pipelined over two steps)
-    const int na = ((d.G + 31) / 32 < 4 ? (d.G + 31) / 32 : 4) + (d.P >= 2 ? 1 : 0);
+    // (+1 compute wave when P >= 2: the update is pipelined over two steps); NAUX does
+    // not depend on C, so neither does the likelihood partition
+    const int na = 1 + (d.P >= 2 ? 1 : 0);
     if (d.W >= na + 2 && d.G <= 128) d.naux = na;
   }
   // rows in LDS when they fit beside the rest of the carve (64 KiB for the rows)
@@ -361,8 +362,9 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   rc |= dalloc(x, &dobs, (size_t)n_obs * n_fields);
   rc |= dalloc(x, &pf, n_params);
   rc |= dalloc(x, &pp, (size_t)8 * n_params);
-  rc |= dalloc(x, &d.vb0, PGC);
-  rc |= dalloc(x, &d.vb1, PGC);
+  // (+128 slack: the Gibbs payload DMA reads whole 64-chain rows of the last group)
+  rc |= dalloc(x, &d.vb0, PGC + 128);
+  rc |= dalloc(x, &d.vb1, PGC + 128);
   rc |= dalloc(x, &d.lp, PGC);
   rc |= dalloc(x, &d.ll, GC);
   rc |= dalloc(x, &d.scale, PGC);
@@ -403,7 +405,7 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   int* dmerge = nullptr;
   rc |= dalloc(x, &dleaf, starts.size());
   rc |= dalloc(x, &dmerge, merges.size());
-  rc |= dalloc(x, &d.cnt, (size_t)32 * d.CB * n_params);
+  rc |= dalloc(x, &d.cnt, (size_t)32 * 8 * d.CB * n_params);   // [CB][P][8 shards][32]
   rc |= dalloc(x, &d.tmo, 4);
   if (rc) { nmc_destroy(x); return rc; }
   d.leaf = dleaf;
@@ -610,7 +612,7 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       if (!partial) {
         if (int rc = launch_run(x, fam, c0, c1, 0)) return rc;
       } else if (x->persistent) {
-        HIPCHK(hipMemsetAsync(x->d.cnt, 0, (size_t)32 * x->d.CB * x->P * sizeof(unsigned),
+        HIPCHK(hipMemsetAsync(x->d.cnt, 0, (size_t)32 * 8 * x->d.CB * x->P * sizeof(unsigned),
                               x->stream));
         if (int rc = launch_run(x, fam, c0, c1, NMC_RUN_HYPER_LOAD)) return rc;
       } else {
