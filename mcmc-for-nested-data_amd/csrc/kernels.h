@@ -116,7 +116,14 @@ struct Dev {
     if (d.stamps && blockIdx.x == 0 && w == 1 && (t) - i0 < 8 && lane == 0)              \
       d.stamps[((0 * 2 + 1) * 8 + ((t) - i0)) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// the compute wave (wave naux) of workgroup 0, into the control-wave row (slots 13-15)
+#define NMC_STAMP_CMP(t, slot)                                                          \
+  do {                                                                                  \
+    if (d.stamps && blockIdx.x == 0 && w == naux && (t) - i0 < 8 && lane == 0)           \
+      d.stamps[((0 * 2 + 0) * 8 + ((t) - i0)) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #else
+#define NMC_STAMP_CMP(t, slot) do {} while (0)
 #define NMC_STAMP_AUX(t, slot) do {} while (0)
 #define NMC_STAMP(t, slot) do {} while (0)
 #define NMC_STAMP_AT(k, slot) do {} while (0)
@@ -728,7 +735,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const bool ctl = w == 0;
   // latency-bound roles (control, loaders, compute) issue ahead of the likelihood waves
   // sharing their SIMD, which fill the gaps
-  if (W > 1 && w <= naux && !(d.noprio)) __builtin_amdgcn_s_setprio(3);
+  if (W > 1 && w <= naux && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
 
   // ---- prologue: values and state -> LDS (parameter p by wave p % W) ----
   const double* vin = ((i0 - 1) & 1) ? d.vb1 : d.vb0;
@@ -961,10 +968,12 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
           }
         } else {   // compute wave: task gs-2, loaded into buffer (gs-2)&1 at step gs-1
           const size_t hvi = (((size_t)(ctq - d.vbase) * P + cq) * C + cc) * 2;
+          if (p == 0) NMC_STAMP_CMP(t, 13);
           nmc_hyper_compute(d, cb, ctq, cq, lds, L, g == 0, d.vh[hvi], d.vh[hvi + 1],
                             (gs & 1) * (G + 1));
+          if (p == 0) NMC_STAMP_CMP(t, 14);
           if (post_prior) step_priors();
-          if (p == 0) NMC_STAMP_AUX(t, 12);
+          if (p == 0) NMC_STAMP_CMP(t, 15);
         }
       }
       // ---- likelihood of the proposal over this wave's rows (:615-635) ----
@@ -1067,9 +1076,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         cwv[NMC_CW_PLL * 64] = llp;
         pend_p = p;
         pend_t = t;
-        // no pooling: the rest waits for the next step's pre-barrier slack; partial pooling:
-        // at once (measured faster: the next step's slack feeds the Gibbs hand-off)
-        if (PARTIAL) apply_pending();
+        // the rest of the update waits for the next step's pre-barrier slack
         if (p == 0) NMC_STAMP(t, 12);
       }
       if (p == 0) NMC_STAMP(t, 3);

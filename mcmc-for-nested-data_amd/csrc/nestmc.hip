@@ -179,7 +179,7 @@ static void choose_geometry(nmc_ctx* x) {
                !(getenv("NMC_NO_LDS_ROWS") && atoi(getenv("NMC_NO_LDS_ROWS")));
   // the persistent Gibbs update by the auxiliary waves needs G <= 128 (one numpy
   // leaf) and one parameter's chain-block values in LDS
-  d.noprio = getenv("NMC_NOPRIO") && atoi(getenv("NMC_NOPRIO"));
+  d.noprio = getenv("NMC_NOPRIO") ? atoi(getenv("NMC_NOPRIO")) : 0;   // diagnostics bits
   d.hlds = d.naux > 0 && d.G <= 128 && lds_bytes_for(x, 1, d.rows_lds) <= (size_t)160 * 1024 &&
            !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
 }

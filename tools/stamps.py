@@ -51,6 +51,10 @@ def main():
                 "hyper_wait_done": [float(x) for x in numpy.median(hy, axis=0)]}
             if ax is not None:   # block 0: auxiliary wave 1 at step 0 (poll, load, join, computed)
                 res["blk0_w1"]["aux_poll_load_join_done"] = [float(x) for x in numpy.median(ax, axis=0)]
+            if (b, wv) == (0, 0):   # block 0: the compute wave at step 0 (start, updated, priors)
+                cx = st[0, 0, 1:7][:, [13, 14, 15]] - st[0, 0, 1:7, 0:1]
+                res["blk0_w0"]["compute_start_done_priors"] = [float(x) for x in
+                                                               numpy.median(cx, axis=0)]
     print(json.dumps(dict(pooling=pooling, N=N, config=eng.launch_config(), stamps=res)))
     eng.close()
 
