@@ -116,10 +116,10 @@ struct Dev {
     if (d.stamps && blockIdx.x == 0 && w == 1 && (t) - i0 < 8 && lane == 0)              \
       d.stamps[((0 * 2 + 1) * 8 + ((t) - i0)) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
-// the compute wave (wave naux) of workgroup 0, into the control-wave row (slots 13-15)
+// compute wave half 0 (wave 1) of workgroup 0, into the control-wave row (slots 13-15)
 #define NMC_STAMP_CMP(t, slot)                                                          \
   do {                                                                                  \
-    if (d.stamps && blockIdx.x == 0 && w == naux && (t) - i0 < 8 && lane == 0)           \
+    if (d.stamps && blockIdx.x == 0 && w == 1 && (t) - i0 < 8 && lane == 0)              \
       d.stamps[((0 * 2 + 0) * 8 + ((t) - i0)) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
@@ -223,7 +223,8 @@ struct nmc_lds_layout {
   int zl;      // [2][2]         {z, log u} of this and the next step (LDS-DMA, step parity)
   int hv;      // [2P]           {hyper z, gamma} of the Gibbs update (LDS-DMA)
   int cw;      // [15]           control-wave temporaries across the step barrier
-  int flag;    // [1]            broadcast word
+  int flag;    // [1]            broadcast / epoch words
+  int xchg;    // [2][8]         stream sums exchanged by the two compute waves
   int rows;    // [nrows_lds][NF] the group's observation rows (staged once per launch)
   int total;   // columns
 };
@@ -242,7 +243,8 @@ __host__ __device__ inline nmc_lds_layout nmc_lds(int nacc, int P, int partial, 
   L.hv = L.zl + 4;
   L.cw = L.hv + (partial ? 2 * P : 0);
   L.flag = L.cw + 15;
-  L.rows = L.flag + 1;
+  L.xchg = L.flag + 1;
+  L.rows = L.xchg + (partial && hlds ? 16 : 0);
   L.total = L.rows + (row_doubles + 63) / 64;
   return L;
 }
@@ -547,6 +549,85 @@ __device__ __forceinline__ void nmc_hyper_compute(const Dev& d, int cb, int t, i
   }
 }
 
+// The same update split over two waves (half 0 / 1 sum numpy streams 0-3 / 4-7 of both
+// leaf sums and swap the stream sums through LDS, so both combine all eight in numpy's
+// order); half 0 finishes and writes.  epoch: unique per task, > every earlier one.
+// Both waves must call it (bounded spins).  Needs G >= 8.
+__device__ __forceinline__ void nmc_hyper_compute2(const Dev& d, int cb, int t, int p, double* lds,
+                                                   const nmc_lds_layout& L, bool write, double hz,
+                                                   double hx, int hoff, int half, double epoch) {
+  const int lane = threadIdx.x & 63;
+  const int P = d.P, G = d.G, C = d.C;
+  const int c = cb * 64 + lane;
+  const double* hv = lds + (size_t)(L.hval + hoff) * 64 + lane;
+  double* hy = lds + L.hyp * 64 + lane;
+  double* xc = lds + (size_t)L.xchg * 64 + lane;
+  double* fl = lds + L.flag * 64 + 16;
+  const double sdm = sqrt(hy[(NMC_HY_S2 * P + p) * 64] / G);
+  const int m8 = G - G % 8;
+  auto leaf = [&](int st, bool sq, double mu) -> double {
+    auto f = [&](int i) -> double {
+      double x = hv[i * 64];
+      if (sq) {
+        x = x - mu;
+        x = x * x;
+      }
+      return x;
+    };
+    double r[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) r[jj] = f(4 * half + jj);
+    for (int i = 8; i < m8; i += 8) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) r[jj] = r[jj] + f(i + 4 * half + jj);
+    }
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) xc[(st * 8 + 4 * half + jj) * 64] = r[jj];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0)
+      __hip_atomic_store(fl + st * 2 + half, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (unsigned spins = 0;
+         __hip_atomic_load(fl + st * 2 + (1 - half), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) !=
+             epoch &&
+         spins < NMC_SPIN_LIMIT;
+         ++spins)
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double rr[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rr[j] = xc[(st * 8 + j) * 64];
+    double res = ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
+    for (int i = m8; i < G; ++i) res += f(i);
+    return res;
+  };
+  const double tot = leaf(0, false, 0.0);
+  const double mu = tot / G + sdm * hz;
+  const double ss = leaf(1, true, mu);
+  if (half != 0) return;
+  const double hat = ss / (double)(G - 1);
+  const double scale = d.ha * hat;
+  const double s2n = scale == 0.0 ? 0.0 : (1.0 / hx) * scale;
+  const double sdn = sqrt(s2n);
+  const double lsd = log(sdn);
+  hy[(NMC_HY_MU * P + p) * 64] = mu;
+  hy[(NMC_HY_SD * P + p) * 64] = sdn;
+  hy[(NMC_HY_LSD * P + p) * 64] = lsd;
+  hy[(NMC_HY_S2 * P + p) * 64] = s2n;
+  hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
+  if (write && c < C) {
+    d.mu[p * C + c] = mu;
+    d.s2[p * C + c] = s2n;
+    d.hsd[p * C + c] = sdn;
+    d.hlsd[p * C + c] = lsd;
+    const int row = nmc_record_row(d, t);
+    if (row >= 0) {
+      double* out = d.samples + ((size_t)row * d.cols + (size_t)p * (G + 2)) * C + c;
+      out[0] = mu;
+      out[C] = s2n;
+    }
+  }
+}
+
 // The calling wave polls the chain block's publish counter until it reaches target
 // (bounded; a timeout is recorded in d.tmo and reported by the host).  The counter is
 // sharded 8 ways (workgroup g adds to shard g % 8, each shard on its own 128-B line)
@@ -621,12 +702,18 @@ __device__ __forceinline__ void nmc_ll_rows(const Fam& fam, const typename Fam::
 // The same over rows staged in LDS: blocks of R rows read with wave-uniform
 // (broadcast) ds_reads; block b+1 is requested before block b is consumed (LDS
 // returns in order, so the wait covers only block b).
+#ifndef NMC_LDS_ROW_DOUBLES
+#define NMC_LDS_ROW_DOUBLES 16   // doubles per software-pipelined LDS block (8 regression rows)
+#endif
 template <class Fam>
 __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename Fam::Reg& reg,
                                                 const double* __restrict__ p, int n,
                                                 double (&acc)[Fam::NACC]) {
   constexpr int NF = Fam::NFIELDS;
-  constexpr int R = (8 / NF) > 0 ? (8 / NF) : 1;
+  // 8-row blocks for 2-field rows (measured: -17 % per iteration for regression),
+  // 8 doubles otherwise (register pressure of the wider families)
+  constexpr int BD = NF <= 2 ? NMC_LDS_ROW_DOUBLES : 8;
+  constexpr int R = (BD / NF) > 0 ? (BD / NF) : 1;
   double a[4][Fam::NACC];
 #pragma unroll
   for (int s = 0; s < 4; ++s)
@@ -851,7 +938,6 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       //      naR, nrR, ta), tuned if due -- parked in LDS (no registers live across
       //      the likelihood region) ----
       if (ctl) {
-        if (pend_p >= 0) apply_pending();
         if constexpr (sync) {   // the previous step's value is stored; count it published
           if (pub_p >= 0) {
             nmc_drain_vm();
@@ -861,6 +947,27 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             pub_p = -1;
           }
         }
+        // P >= 2: the control wave is the loader, right after its own publish (the copies
+        // stay in flight under the rest of its pre-barrier work): it waits for the chain
+        // block's counter of task gs-1 (verdict word for the check after barrier A) and
+        // copies the payload into LDS buffer (gs-1)&1 (sc1 LDS-DMA, drained with its other
+        // copies before barrier A)
+        if constexpr (hl) if (pipe && aux_now) {
+          const bool r = nmc_poll_published(d, cb, aq, (unsigned)G * (unsigned)(atq - i0 + 1));
+          if (lane == 0)
+            __hip_atomic_store(lds + L.flag * 64 + 1, r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (p == 0) NMC_STAMP(t, 8);
+          if (r) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const double* src = (atq & 1) ? d.vb1 : d.vb0;
+            if ((C & 1) == 0)
+              nmc_hyper_dma(d, src, aq, cb, 0, G, lds, L, ((gs - 1) & 1) * (G + 1));
+            else
+              nmc_hyper_load(d, src, aq, cc, 0, G, lds, L, ((gs - 1) & 1) * (G + 1));
+          }
+        }
+        if (pend_p >= 0) apply_pending();
         {
           const double na = st[(NMC_ST_NA * P + p) * 64], nr = st[(NMC_ST_NR * P + p) * 64];
           double sA = s, sR = s, naA = na + 1.0, nrA = nr, naR = na, nrR = nr + 1.0;
@@ -905,7 +1012,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       //      through LDS epoch words and wave 1 computes; P >= 2: the compute wave (the
       //      last auxiliary) updates task gs-2 from the buffer the loaders filled at the
       //      previous step ----
-      const int nload = pipe ? naux - 1 : naux;
+      const int nload = pipe ? 0 : naux;   // P >= 2: the control wave loads, waves 1-2 compute
       const bool aux = hl && w >= 1 && w <= naux && (w <= nload ? aux_now : comp_now);
       if constexpr (hl) if (aux) {
         const int a = w - 1;
@@ -966,13 +1073,18 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
               }
             }
           }
-        } else {   // compute wave: task gs-2, loaded into buffer (gs-2)&1 at step gs-1
+        } else {   // compute waves: task gs-2, loaded into buffer (gs-2)&1 at step gs-1
+          const int half = w - nload - 1;
           const size_t hvi = (((size_t)(ctq - d.vbase) * P + cq) * C + cc) * 2;
           if (p == 0) NMC_STAMP_CMP(t, 13);
-          nmc_hyper_compute(d, cb, ctq, cq, lds, L, g == 0, d.vh[hvi], d.vh[hvi + 1],
-                            (gs & 1) * (G + 1));
+          if (G >= 8)
+            nmc_hyper_compute2(d, cb, ctq, cq, lds, L, g == 0, d.vh[hvi], d.vh[hvi + 1],
+                               (gs & 1) * (G + 1), half, (double)(gs + 1));
+          else if (half == 0)
+            nmc_hyper_compute(d, cb, ctq, cq, lds, L, g == 0, d.vh[hvi], d.vh[hvi + 1],
+                              (gs & 1) * (G + 1));
           if (p == 0) NMC_STAMP_CMP(t, 14);
-          if (post_prior) step_priors();
+          if (post_prior && half == 0) step_priors();
           if (p == 0) NMC_STAMP_CMP(t, 15);
         }
       }
@@ -1113,7 +1225,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   if constexpr (hl) if (ok && g == 0) {
     const int ge = i1 * P;   // tasks ge-2 (loaded at the last step; P >= 2) and ge-1 are left
     const bool pipe = P >= 2;
-    const int nload = pipe ? naux - 1 : naux;
+    const int nload = 1;   // closing: wave 1 loads
     if (pipe && w == naux) {
       const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 2)) * C + cc) * 2;
       nmc_hyper_compute(d, cb, i1 - 1, P - 2, lds, L, true, d.vh[hvi], d.vh[hvi + 1],

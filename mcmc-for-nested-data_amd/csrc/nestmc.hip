@@ -163,14 +163,15 @@ static void choose_geometry(nmc_ctx* x) {
     if (v >= 1 && v <= 16) w = v;
   }
   d.W = (int)w;
-  // partial pooling: one loader wave (the payload is LDS-DMA, no registers) + one
-  // compute wave when P >= 2; reserved in every partial mode so the likelihood
+  // partial pooling: P >= 2: two compute waves (the control wave loads the payload
+  // by LDS-DMA); P == 1: one wave loads and computes; reserved in every partial mode so the likelihood
   // partition (W - 1 - NAUX waves) is the same whatever the launch mode
   d.naux = 0;
   if (x->pooling == NMC_POOL_PARTIAL) {
-    // (+1 compute wave when P >= 2: the update is pipelined over two steps); NAUX does
+    // (+2 compute waves when P >= 2: the update is pipelined over two steps and split
+    // over two waves); NAUX does
     // not depend on C, so neither does the likelihood partition
-    const int na = 1 + (d.P >= 2 ? 1 : 0);
+    const int na = d.P >= 2 ? 2 : 1;
     if (d.W >= na + 2 && d.G <= 128) d.naux = na;
   }
   // rows in LDS when they fit beside the rest of the carve (64 KiB for the rows)

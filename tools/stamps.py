@@ -55,6 +55,8 @@ def main():
                 cx = st[0, 0, 1:7][:, [13, 14, 15]] - st[0, 0, 1:7, 0:1]
                 res["blk0_w0"]["compute_start_done_priors"] = [float(x) for x in
                                                                numpy.median(cx, axis=0)]
+                res["blk0_w0"]["cw_poll_done"] = float(numpy.median(st[0, 0, 1:7, 8] -
+                                                                st[0, 0, 1:7, 0]))
     print(json.dumps(dict(pooling=pooling, N=N, config=eng.launch_config(), stamps=res)))
     eng.close()
 
