@@ -141,8 +141,13 @@ int nmc_write_ll_csv(const char* path, int append, const double* ll, int64_t n,
 int nmc_comm_unique_id(unsigned char* out /* 128 bytes */);
 int nmc_comm_init(void** comm, const unsigned char* id, int nranks, int rank, int device);
 int nmc_comm_destroy(void* comm);
-/* root receives [rank][row][col][C_local] (all ranks must have equal C_local). */
-int nmc_gather_samples(nmc_ctx* ctx, void* comm, int root, double* host_out);
+/* Rank count and this rank's id of a communicator (ncclCommCount/UserRank). */
+int nmc_comm_size(void* comm, int* nranks, int* rank);
+/* root receives [rank][row][col][C_local] (all ranks must have equal C_local) in
+ * host_out, which must hold host_capacity >= nranks * rows * cols * C_local doubles
+ * (ignored on the other ranks, which may pass NULL).                            */
+int nmc_gather_samples(nmc_ctx* ctx, void* comm, int root, double* host_out,
+                       int64_t host_capacity);
 
 /* Verification hooks (tests only): device numerics on caller inputs.
  *   prior logpdf of family fam with params[8] at xs[n]   (scipy .logpdf)

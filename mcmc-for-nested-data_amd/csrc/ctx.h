@@ -1,0 +1,113 @@
+// ctx.h -- libnestmc internals shared by the C-ABI (nestmc.hip) and the per-family
+// translation units (fam_*.hip): the context, error plumbing, the LDS/geometry helpers
+// and the family dispatch table.
+//
+// The kernels are templates over the likelihood family (families.h); instantiating all
+// of them for every family and row width in one translation unit took ~90 s, so each
+// family lives in its own TU (built in parallel) and is reached through nmc_call_*().
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/nestmc.h"
+#include "kernels.h"
+
+// error message of the calling thread (nestmc.hip); returns code
+int nmc_fail(int code, const std::string& msg);
+
+#define HIPCHK(x)                                                                     \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess)                                                             \
+      return nmc_fail(-2, std::string(#x) + ": " + hipGetErrorString(e_));            \
+  } while (0)
+
+struct nmc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int C = 0, chain_base = 0, G = 0, P = 0, pooling = 0, family = 0, nf = 0, rng = 0;
+  uint32_t seed = 0;
+  int64_t n_obs = 0;
+  std::vector<double> llc;
+  Dev d{};
+  std::vector<void*> owned;
+  int n_iter = 0;
+  bool scheduled = false;
+  bool trace = false;
+  hipEvent_t ev[16] = {};
+  bool ktiming = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> kev;   // step launches
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> hev;   // hyper-only launches
+  size_t kev_used = 0, hev_used = 0;
+  double step_ms = 0, hyper_ms = 0;
+  long long step_n = 0, hyper_n = 0;
+  long long step_iters = 0;
+  int launch_iters = 0;                    // cap on iterations per launch (0: vcap)
+  std::vector<int> kev_iters;             // iterations covered by each timed step launch
+  int cur_slot = 1;                       // state after the last iteration: slot cur_slot
+  int nacc = 1;                           // likelihood accumulators of the family
+  bool persistent = false;                // partial pooling: one resident launch per chunk
+  int ncu = 256;
+};
+
+static inline double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->d.vb0; }
+
+static inline size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
+  const Dev& d = x->d;
+  return (size_t)nmc_lds(x->nacc, d.P, x->pooling == NMC_POOL_PARTIAL, d.nleaf, d.ntail, d.W,
+                         d.G, hlds, rows_lds ? d.nmax * x->nf : 0)
+             .total * 512;
+}
+static inline size_t run_lds_bytes(const nmc_ctx* x) {
+  return lds_bytes_for(x, x->persistent && x->d.hlds ? 1 : 0, x->d.rows_lds);
+}
+
+static inline int run_mode(const nmc_ctx* x) {
+  if (x->pooling != NMC_POOL_PARTIAL) return NMC_MODE_NOPOOL;
+  if (!x->persistent) return NMC_MODE_LAUNCH;
+  return x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
+}
+
+static inline int pop_event_pair(nmc_ctx* x, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v,
+                                 size_t& used, std::pair<hipEvent_t, hipEvent_t>** out) {
+  if (used == v.size()) {
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    v.emplace_back(a, b);
+  }
+  *out = &v[used++];
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// family dispatch: one entry per family TU; op selects what to launch
+// ---------------------------------------------------------------------------
+enum {
+  NMC_OP_RUN = 0,          // step kernel over iterations [i0, i1) with flags
+  NMC_OP_CAN_PERSIST = 1,  // result = 1 if the persistent grid is co-resident
+  NMC_OP_GROUP_LL = 2,     // in = theta [P][G][C] (device), out = [G][C] (device)
+  NMC_OP_OBS_LL = 3        // in = values [P][G][C] (device), out = [C][n_obs] (device)
+};
+struct NmcCall {
+  int op = 0;
+  int i0 = 0, i1 = 0, flags = 0;
+  const double* in = nullptr;
+  double* out = nullptr;
+  int result = 0;
+};
+int nmc_call_linreg(nmc_ctx* x, NmcCall& c);
+int nmc_call_gauss_mean(nmc_ctx* x, NmcCall& c);
+int nmc_call_logistic(nmc_ctx* x, NmcCall& c);
+
+static inline int nmc_call_family(nmc_ctx* x, NmcCall& c) {
+  switch (x->family) {
+    case NMC_LL_LINREG: return nmc_call_linreg(x, c);
+    case NMC_LL_GAUSS_MEAN: return nmc_call_gauss_mean(x, c);
+    case NMC_LL_LOGISTIC: return nmc_call_logistic(x, c);
+  }
+  return nmc_fail(-1, "unknown likelihood family");
+}

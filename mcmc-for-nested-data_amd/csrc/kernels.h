@@ -59,7 +59,7 @@ struct Dev {
   int* nacc;             // [P][G][C]  since last tune
   int* nrej;
   long long* tacc;       // [P][G][C]  total accepted
-  double* mu;            // [P][C]
+  double* mu;            // [2][P][C]: after iteration t in slot t & 1 (nmc_hslot)
   double* s2;
   double* hsd;           // sqrt(s2)
   double* hlsd;          // log(sqrt(s2))
@@ -132,6 +132,12 @@ struct Dev {
 enum { NMC_RUN_HYPER_LOAD = 1 };
 enum { NMC_SPIN_LIMIT = 1 << 22 };
 
+// Offset of the hyper-parameter slot holding the state after iteration t ([2][P][C]:
+// slot t & 1, like the values vb[t & 1]); a launch reads one slot and writes the other.
+__device__ __forceinline__ size_t nmc_hslot(const Dev& d, int t) {
+  return (size_t)(t & 1) * d.P * d.C;
+}
+
 __device__ __forceinline__ int nmc_record_row(const Dev& d, int iter) {
   if (iter < d.burn || (iter % d.thin) != 0) return -1;
   const int first = ((d.burn + d.thin - 1) / d.thin) * d.thin;
@@ -155,58 +161,6 @@ __device__ __forceinline__ void nmc_tune(double& s, double& na, double& nr) {
   na = 0.0;
   nr = 0.0;
   if (ns != 0.0) s = ns;
-}
-
-// ---------------------------------------------------------------------------
-// Variates for iterations [iter0, iter0 + T): one thread per (t, p, g, c) element
-// of the step variates and per (t, p, c) of the hyper variates.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) nmc_k_fill(Dev d, int iter0, int T) {
-  const size_t PGC = (size_t)d.P * d.G * d.C, PC = (size_t)d.P * d.C;
-  const size_t n1 = (size_t)T * PGC;
-  const size_t n2 = d.pooling == NMC_POOL_PARTIAL ? (size_t)T * PC : 0;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n1 + n2;
-       i += (size_t)gridDim.x * blockDim.x) {
-    if (i < n1) {
-      const int t = (int)(i / PGC);
-      const size_t r = i % PGC;
-      const int c = (int)(r % d.C);
-      const int g = (int)((r / d.C) % d.G);
-      const int p = (int)(r / ((size_t)d.C * d.G));
-      const int it = iter0 + t;
-      double z, lu;
-      if (d.rng_mode == NMC_RNG_REPLAY) {
-        const size_t k = (size_t)it * PGC + r;
-        z = it < d.replay_n ? d.rz[k] : nmc_nan();
-        lu = it < d.replay_n ? log(d.ru[k]) : nmc_nan();
-      } else {
-        const uint32_t ch = (uint32_t)(d.chain_base + c);
-        z = nmc_normal(it, g, p, NMC_PURPOSE_PROPOSAL, ch, d.seed);
-        lu = log(nmc_uniform2(it, g, p, NMC_PURPOSE_ACCEPT, ch, d.seed).a);
-      }
-      d.vzl[2 * i] = z;
-      d.vzl[2 * i + 1] = lu;
-    } else {
-      const size_t j = i - n1;
-      const int t = (int)(j / PC);
-      const size_t r = j % PC;
-      const int c = (int)(r % d.C);
-      const int p = (int)(r / d.C);
-      const int it = iter0 + t;
-      double hz, hx;
-      if (d.rng_mode == NMC_RNG_REPLAY) {
-        const size_t k = (size_t)it * PC + r;
-        hz = it < d.replay_n ? d.rhz[k] : nmc_nan();
-        hx = it < d.replay_n ? nmc_igamci(d.ha, d.rhu[k], d.hlga) : nmc_nan();
-      } else {
-        const uint32_t ch = (uint32_t)(d.chain_base + c);
-        hz = nmc_normal(it, 0, p, NMC_PURPOSE_HYPER_NORMAL, ch, d.seed);
-        hx = nmc_gamma_mt(d.ha, it, p, ch, d.seed);
-      }
-      d.vh[2 * j] = hz;
-      d.vh[2 * j + 1] = hx;
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -422,10 +376,11 @@ __device__ __forceinline__ void nmc_hyper(const Dev& d, const double* src, int c
     lds[(L.hyp + NMC_HY_S2 * P + p) * 64 + lane] = s2n;
     lds[(L.hyp + NMC_HY_ISD * P + p) * 64 + lane] = 1.0 / sdn;
     if (write && c < C) {
-      d.mu[p * C + c] = m;
-      d.s2[p * C + c] = s2n;
-      d.hsd[p * C + c] = sdn;
-      d.hlsd[p * C + c] = lsd;
+      const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
+      d.mu[ho] = m;
+      d.s2[ho] = s2n;
+      d.hsd[ho] = sdn;
+      d.hlsd[ho] = lsd;
       if (row >= 0) {
         double* out = d.samples + ((size_t)row * d.cols + (size_t)p * (G + 2)) * C + c;
         out[0] = m;
@@ -536,10 +491,11 @@ __device__ __forceinline__ void nmc_hyper_compute(const Dev& d, int cb, int t, i
   hy[(NMC_HY_S2 * P + p) * 64] = s2n;
   hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
   if (write && c < C) {
-    d.mu[p * C + c] = mu;
-    d.s2[p * C + c] = s2n;
-    d.hsd[p * C + c] = sdn;
-    d.hlsd[p * C + c] = lsd;
+    const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
+    d.mu[ho] = mu;
+    d.s2[ho] = s2n;
+    d.hsd[ho] = sdn;
+    d.hlsd[ho] = lsd;
     const int row = nmc_record_row(d, t);
     if (row >= 0) {
       double* out = d.samples + ((size_t)row * d.cols + (size_t)p * (G + 2)) * C + c;
@@ -615,10 +571,11 @@ __device__ __forceinline__ void nmc_hyper_compute2(const Dev& d, int cb, int t, 
   hy[(NMC_HY_S2 * P + p) * 64] = s2n;
   hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
   if (write && c < C) {
-    d.mu[p * C + c] = mu;
-    d.s2[p * C + c] = s2n;
-    d.hsd[p * C + c] = sdn;
-    d.hlsd[p * C + c] = lsd;
+    const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
+    d.mu[ho] = mu;
+    d.s2[ho] = s2n;
+    d.hsd[ho] = sdn;
+    d.hlsd[ho] = lsd;
     const int row = nmc_record_row(d, t);
     if (row >= 0) {
       double* out = d.samples + ((size_t)row * d.cols + (size_t)p * (G + 2)) * C + c;
@@ -835,13 +792,18 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     st[(NMC_ST_NR * P + p) * 64] = (double)d.nrej[ip];
     st[(NMC_ST_TA * P + p) * 64] = (double)d.tacc[ip];
     if (PARTIAL) {
-      const double s2 = d.s2[p * C + cc];
-      hy[(NMC_HY_MU * P + p) * 64] = d.mu[p * C + cc];
-      hy[(NMC_HY_SD * P + p) * 64] = d.hsd[p * C + cc];
-      hy[(NMC_HY_LSD * P + p) * 64] = d.hlsd[p * C + cc];
+      // hyper-parameters after iteration i0-1 (chunk start), or after i0-2 when this
+      // launch recomputes the update after i0-1 at step 0 (launch per iteration): that
+      // update is written to the other slot, so no workgroup of this launch can read it
+      const size_t ho =
+          nmc_hslot(d, (flags & NMC_RUN_HYPER_LOAD) ? i0 - 1 : i0 - 2) + (size_t)p * C + cc;
+      const double s2 = d.s2[ho];
+      hy[(NMC_HY_MU * P + p) * 64] = d.mu[ho];
+      hy[(NMC_HY_SD * P + p) * 64] = d.hsd[ho];
+      hy[(NMC_HY_LSD * P + p) * 64] = d.hlsd[ho];
       hy[(NMC_HY_S2 * P + p) * 64] = s2;
       hy[(NMC_HY_SDM * P + p) * 64] = sqrt(s2 / G);
-      hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / d.hsd[p * C + cc];
+      hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / d.hsd[ho];
     }
   }
   const double gcst = fam.gconst((long)nrow);   // per-group constant of finish_fast
@@ -1259,28 +1221,6 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   }
 }
 
-// Gibbs update after iteration t alone (closes a chunk in launch-per-iteration mode);
-// grid = CB workgroups.
-__global__ void __launch_bounds__(1024) nmc_k_hyper(Dev d, const double* src, int t) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int W = blockDim.x >> 6;
-  const int P = d.P, C = d.C;
-  const int c = blockIdx.x * 64 + lane;
-  const int cc = c < C ? c : C - 1;
-  const nmc_lds_layout L = nmc_lds(0, P, 1, d.nleaf, d.ntail, 0, d.G, 0);
-  for (int p = w; p < P; p += W) {
-    const double s2 = d.s2[p * C + cc];
-    lds[(L.hyp + NMC_HY_S2 * P + p) * 64 + lane] = s2;
-    lds[(L.hyp + NMC_HY_SDM * P + p) * 64 + lane] = sqrt(s2 / d.G);
-  }
-  nmc_hyper_variates(d, blockIdx.x, t, lds, L, 0, W);
-  nmc_drain_vm();
-  __syncthreads();
-  nmc_hyper<NMC_SRC_GLOBAL>(d, src, blockIdx.x, t, lds, L, true);
-}
-
 // Group sums for arbitrary theta [P][G][C] -> out [G][C] (all W waves stream rows).
 template <class Fam>
 __global__ void __launch_bounds__(1024)
@@ -1333,29 +1273,3 @@ nmc_k_obs_ll(Dev d, Fam fam, const double* value, double* out, int64_t n_obs) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// debug/verification kernels (device numerics against scipy / the oracle)
-// ---------------------------------------------------------------------------
-__global__ void nmc_k_debug_prior(int fam, const double* prm, const double* x, int n, double* out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = nmc_prior_logpdf(fam, prm, x[i]);
-}
-
-__global__ void nmc_k_debug_igamci(const double* a, const double* q, const double* lga, int n,
-                                   double* out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = nmc_igamci(a[i], q[i], lga[i]);
-}
-
-// out[i] = {normal(purpose), uniform a, uniform b, gamma_mt(a)} for counters in ctr[i][5]
-// = (iter, group, param, purpose, chain); gamma uses (iter, param, chain).
-__global__ void nmc_k_debug_rng(const uint32_t* ctr, int n, uint32_t seed, double ga, double* out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t* k = ctr + 5 * i;
-  const nmc_d2 u = nmc_uniform2(k[0], k[1], k[2], k[3], k[4], seed);
-  out[4 * i + 0] = nmc_box_muller(u.a, u.b);
-  out[4 * i + 1] = u.a;
-  out[4 * i + 2] = u.b;
-  out[4 * i + 3] = nmc_gamma_mt(ga, k[0], k[2], k[4], seed);
-}

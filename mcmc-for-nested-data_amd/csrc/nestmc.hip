@@ -17,54 +17,18 @@
 #include <vector>
 #include <algorithm>
 
-#include "../../include/nestmc.h"
-#include "kernels.h"
+#include "ctx.h"
+#include "kernels_misc.h"
 
-#define NMC_VERSION "nestmc 0.1.0 (gfx950)"
+#define NMC_VERSION "nestmc 0.2.0 (gfx950)"
 
 static thread_local std::string g_err;
 
-static int fail(int code, const std::string& msg) {
+int nmc_fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
-
-#define HIPCHK(x)                                                                     \
-  do {                                                                                \
-    hipError_t e_ = (x);                                                              \
-    if (e_ != hipSuccess)                                                             \
-      return fail(-2, std::string(#x) + ": " + hipGetErrorString(e_));                \
-  } while (0)
-
-struct nmc_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  int C = 0, chain_base = 0, G = 0, P = 0, pooling = 0, family = 0, nf = 0, rng = 0;
-  uint32_t seed = 0;
-  int64_t n_obs = 0;
-  std::vector<double> llc;
-  Dev d{};
-  std::vector<void*> owned;
-  int n_iter = 0;
-  bool scheduled = false;
-  bool trace = false;
-  hipEvent_t ev[16] = {};
-  bool ktiming = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> kev;   // step launches
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> hev;   // hyper-only launches
-  size_t kev_used = 0, hev_used = 0;
-  double step_ms = 0, hyper_ms = 0;
-  long long step_n = 0, hyper_n = 0;
-  long long step_iters = 0;
-  int launch_iters = 0;                    // cap on iterations per launch (0: vcap)
-  std::vector<int> kev_iters;             // iterations covered by each timed step launch
-  int cur_slot = 1;                       // values after the last iteration: vb[cur_slot]
-  int nacc = 1;                           // likelihood accumulators of the family
-  bool persistent = false;                // partial pooling: one resident launch per chunk
-  int ncu = 256;
-};
-
-static double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->d.vb0; }
+static int fail(int code, const std::string& msg) { return nmc_fail(code, msg); }
 
 template <class T>
 static int dalloc(nmc_ctx* x, T** p, size_t n) {
@@ -80,73 +44,6 @@ static void dfree(nmc_ctx* x, void* p) {
   if (!p) return;
   for (auto& q : x->owned)
     if (q == p) { hipFree(q); q = nullptr; }
-}
-
-// ---------------------------------------------------------------------------
-// family dispatch: (family, n_fields) -> concrete functor type
-// ---------------------------------------------------------------------------
-template <int NF>
-static FamLinreg<NF> make_linreg(const std::vector<double>& c) {
-  FamLinreg<NF> f{};
-  f.intercept = (int)c[1];
-  f.sigma_known = c[2];
-  f.log_sigma_known = c.size() > 3 ? c[3] : 0.0;
-  f.inv_s2_known = c[2] > 0 ? 1.0 / (c[2] * c[2]) : 0.0;
-  return f;
-}
-template <int NF>
-static FamGaussMean<NF> make_gauss(const std::vector<double>& c) {
-  FamGaussMean<NF> f{};
-  f.bad = 0;
-  for (int j = 0; j < NF; ++j) {
-    f.sd[j] = c[j];
-    f.lsd[j] = c[NF + j];
-    f.isd2[j] = 1.0 / (c[j] * c[j]);
-    if (!(c[j] > 0.0)) f.bad = 1;
-  }
-  return f;
-}
-template <int NF>
-static FamLogistic<NF> make_logistic(const std::vector<double>& c) {
-  FamLogistic<NF> f{};
-  f.intercept = (int)c[1];
-  return f;
-}
-
-template <int NF, class Fn>
-static int with_nf(nmc_ctx* x, Fn&& fn) {
-  switch (x->family) {
-    case NMC_LL_LINREG: return fn(make_linreg<NF>(x->llc));
-    case NMC_LL_GAUSS_MEAN: return fn(make_gauss<NF>(x->llc));
-    case NMC_LL_LOGISTIC: return fn(make_logistic<NF>(x->llc));
-  }
-  return fail(-1, "unknown likelihood family");
-}
-
-template <class Fn>
-static int with_family(nmc_ctx* x, Fn&& fn) {
-  switch (x->nf) {
-    case 1: return with_nf<1>(x, fn);
-    case 2: return with_nf<2>(x, fn);
-    case 3: return with_nf<3>(x, fn);
-    case 4: return with_nf<4>(x, fn);
-    case 5: return with_nf<5>(x, fn);
-    case 6: return with_nf<6>(x, fn);
-    case 7: return with_nf<7>(x, fn);
-    case 8: return with_nf<8>(x, fn);
-    case 9: return with_nf<9>(x, fn);
-  }
-  return fail(-1, "n_fields must be 1..9");
-}
-
-static size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
-  const Dev& d = x->d;
-  return (size_t)nmc_lds(x->nacc, d.P, x->pooling == NMC_POOL_PARTIAL, d.nleaf, d.ntail, d.W,
-                         d.G, hlds, rows_lds ? d.nmax * x->nf : 0)
-             .total * 512;
-}
-static size_t run_lds_bytes(const nmc_ctx* x) {
-  return lds_bytes_for(x, x->persistent && x->d.hlds ? 1 : 0, x->d.rows_lds);
 }
 
 // Waves per workgroup from the rows per group only (>= 64 rows per likelihood wave,
@@ -185,18 +82,6 @@ static void choose_geometry(nmc_ctx* x) {
            !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
 }
 
-static int pop_event_pair(nmc_ctx* x, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v,
-                          size_t& used, std::pair<hipEvent_t, hipEvent_t>** out) {
-  if (used == v.size()) {
-    hipEvent_t a, b;
-    HIPCHK(hipEventCreate(&a));
-    HIPCHK(hipEventCreate(&b));
-    v.emplace_back(a, b);
-  }
-  *out = &v[used++];
-  return 0;
-}
-
 // numpy's pairwise-sum recursion over G groups (numpy/_core/src/umath/loops_utils.h):
 // leaves of <= 128 elements in order, and the post-order merges of their sums.
 static int pairwise_plan(int s, int n, std::vector<int>& starts, std::vector<int>& merges) {
@@ -213,47 +98,6 @@ static int pairwise_plan(int s, int n, std::vector<int>& starts, std::vector<int
   return a;
 }
 
-static int run_mode(const nmc_ctx* x) {
-  if (x->pooling != NMC_POOL_PARTIAL) return NMC_MODE_NOPOOL;
-  if (!x->persistent) return NMC_MODE_LAUNCH;
-  return x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
-}
-
-// Iterations [i0, i1) of the step kernel (one launch).
-template <class Fam>
-static int launch_run(nmc_ctx* x, const Fam& fam, int i0, int i1, int flags) {
-  Dev& d = x->d;
-  const size_t lds = run_lds_bytes(x);
-  std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
-  if (x->ktiming) {
-    if (int rc = pop_event_pair(x, x->kev, x->kev_used, &ev)) return rc;
-    if (x->kev_iters.size() < x->kev_used) x->kev_iters.resize(x->kev_used);
-    x->kev_iters[x->kev_used - 1] = i1 - i0;
-    HIPCHK(hipEventRecord(ev->first, x->stream));
-  }
-  const dim3 grid(d.CB * d.G), block(64 * d.W);
-  switch (run_mode(x)) {
-    case NMC_MODE_NOPOOL:
-      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_NOPOOL>), grid, block, lds, x->stream, d, fam,
-                         d.obs, i0, i1, flags);
-      break;
-    case NMC_MODE_LAUNCH:
-      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_LAUNCH>), grid, block, lds, x->stream, d, fam,
-                         d.obs, i0, i1, flags);
-      break;
-    case NMC_MODE_SYNC:
-      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC>), grid, block, lds, x->stream, d, fam,
-                         d.obs, i0, i1, flags);
-      break;
-    default:
-      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC_LDS>), grid, block, lds, x->stream, d, fam,
-                         d.obs, i0, i1, flags);
-  }
-  HIPCHK(hipGetLastError());
-  if (ev) HIPCHK(hipEventRecord(ev->second, x->stream));
-  return 0;
-}
-
 // Gibbs update after iteration t alone (closes a chunk in launch-per-iteration mode).
 static int launch_hyper(nmc_ctx* x, int t) {
   std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
@@ -268,23 +112,6 @@ static int launch_hyper(nmc_ctx* x, int t) {
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev->second, x->stream));
   return 0;
-}
-
-// Partial pooling: may every workgroup of the grid be resident at once?  (The
-// persistent kernel's chain-block waits need it.)  One block of margin per CU where
-// the occupancy query can over-report (MI355X_MICROARCH.md, residency).
-template <class Fam>
-static bool can_persist(nmc_ctx* x) {
-  if (const char* e = getenv("NMC_PERSIST")) return atoi(e) != 0;
-  int nb = 0;
-  const void* k = x->d.hlds ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_LDS>
-                            : (const void*)nmc_k_run<Fam, NMC_MODE_SYNC>;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W,
-                                                   lds_bytes_for(x, x->d.hlds, x->d.rows_lds)) !=
-      hipSuccess)
-    return false;
-  const int safe = nb > 1 ? nb - 1 : nb;
-  return (int64_t)x->d.CB * x->d.G <= (int64_t)safe * x->ncu;
 }
 
 static int check_timeout(nmc_ctx* x) {
@@ -372,10 +199,11 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   rc |= dalloc(x, &d.nacc, PGC);
   rc |= dalloc(x, &d.nrej, PGC);
   rc |= dalloc(x, &d.tacc, PGC);
-  rc |= dalloc(x, &d.mu, PC);
-  rc |= dalloc(x, &d.s2, PC);
-  rc |= dalloc(x, &d.hsd, PC);
-  rc |= dalloc(x, &d.hlsd, PC);
+  // hyper-parameters after iteration t live in slot t & 1 ([2][P][C]), like the values
+  rc |= dalloc(x, &d.mu, 2 * PC);
+  rc |= dalloc(x, &d.s2, 2 * PC);
+  rc |= dalloc(x, &d.hsd, 2 * PC);
+  rc |= dalloc(x, &d.hlsd, 2 * PC);
   if (rc) { nmc_destroy(x); return rc; }
   d.off = off; d.obs = dobs; d.pfam = pf; d.ppar = pp;
   d.C = n_chains; d.G = n_groups; d.P = n_params; d.pooling = pooling; d.nf = n_fields;
@@ -425,8 +253,12 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     return fail(-1, "workgroup state exceeds the 160 KiB LDS of a CU (too many parameters, "
                     "groups or rows per group)");
   }
-  if (pooling == NMC_POOL_PARTIAL)
-    x->persistent = with_family(x, [&](auto fam) -> int { return can_persist<decltype(fam)>(x) ? 1 : 0; }) == 1;
+  if (pooling == NMC_POOL_PARTIAL) {
+    NmcCall c;
+    c.op = NMC_OP_CAN_PERSIST;
+    if (int rc2 = nmc_call_family(x, c)) { nmc_destroy(x); return rc2; }
+    x->persistent = c.result == 1;
+  }
   d.thin = 1; d.tune_interval = 100;
   HIPCHK(hipMemcpy(off, group_offsets, (n_groups + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
   if (n_obs > 0)
@@ -468,10 +300,11 @@ int nmc_set_state(nmc_ctx* x, const double* value, const double* log_prior, cons
     if (!hyper_mu || !hyper_sigma2) return fail(-1, "partial pooling needs hyper_mu/hyper_sigma2");
     std::vector<double> sd(PC), lsd(PC);
     for (size_t i = 0; i < PC; ++i) { sd[i] = sqrt(hyper_sigma2[i]); lsd[i] = log(sd[i]); }
-    HIPCHK(hipMemcpy(d.mu, hyper_mu, PC * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(d.s2, hyper_sigma2, PC * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(d.hsd, sd.data(), PC * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(d.hlsd, lsd.data(), PC * 8, hipMemcpyHostToDevice));
+    // the state "after iteration -1" lives in slot 1 (values: vb1)
+    HIPCHK(hipMemcpy(d.mu + PC, hyper_mu, PC * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d.s2 + PC, hyper_sigma2, PC * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d.hsd + PC, sd.data(), PC * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d.hlsd + PC, lsd.data(), PC * 8, hipMemcpyHostToDevice));
   }
   if (scale) {
     HIPCHK(hipMemcpy(d.scale, scale, PGC * 8, hipMemcpyHostToDevice));
@@ -494,8 +327,9 @@ int nmc_get_state(nmc_ctx* x, double* value, double* log_prior, double* ll, doub
   if (value) HIPCHK(hipMemcpy(value, vslot(x, x->cur_slot), PGC * 8, hipMemcpyDeviceToHost));
   if (log_prior) HIPCHK(hipMemcpy(log_prior, d.lp, PGC * 8, hipMemcpyDeviceToHost));
   if (ll) HIPCHK(hipMemcpy(ll, d.ll, GC * 8, hipMemcpyDeviceToHost));
-  if (hyper_mu) HIPCHK(hipMemcpy(hyper_mu, d.mu, PC * 8, hipMemcpyDeviceToHost));
-  if (hyper_sigma2) HIPCHK(hipMemcpy(hyper_sigma2, d.s2, PC * 8, hipMemcpyDeviceToHost));
+  const size_t ho = (size_t)x->cur_slot * PC;
+  if (hyper_mu) HIPCHK(hipMemcpy(hyper_mu, d.mu + ho, PC * 8, hipMemcpyDeviceToHost));
+  if (hyper_sigma2) HIPCHK(hipMemcpy(hyper_sigma2, d.s2 + ho, PC * 8, hipMemcpyDeviceToHost));
   if (scale) HIPCHK(hipMemcpy(scale, d.scale, PGC * 8, hipMemcpyDeviceToHost));
   return 0;
 }
@@ -590,6 +424,11 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
   if (iter_begin == iter_end) return 0;
   if (x->rng == NMC_RNG_REPLAY && (!x->d.rz || iter_end > x->d.replay_n))
     return fail(-1, "replay variates do not cover the iteration range");
+  {   // a persistent launch that already timed out: stop before queueing more work
+    unsigned t = 0;
+    if (hipMemcpy(&t, x->d.tmo, sizeof(t), hipMemcpyDeviceToHost) == hipSuccess && t)
+      return check_timeout(x);
+  }
   const bool partial = x->pooling == NMC_POOL_PARTIAL;
   const int P = x->P;
   // the kernels read the values after iteration iter_begin-1 from vb[(iter_begin-1)&1]
@@ -597,9 +436,23 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
   if (x->cur_slot != need) {
     HIPCHK(hipMemcpyAsync(vslot(x, need), vslot(x, x->cur_slot),
                           (size_t)x->P * x->G * x->C * 8, hipMemcpyDeviceToDevice, x->stream));
+    if (partial) {
+      const size_t PC = (size_t)x->P * x->C;
+      for (double* h : {x->d.mu, x->d.s2, x->d.hsd, x->d.hlsd})
+        HIPCHK(hipMemcpyAsync(h + need * PC, h + x->cur_slot * PC, PC * 8,
+                              hipMemcpyDeviceToDevice, x->stream));
+    }
     x->cur_slot = need;
   }
-  int rc = with_family(x, [&](auto fam) -> int {
+  auto launch_run = [&](int i0, int i1, int flags) -> int {
+    NmcCall c;
+    c.op = NMC_OP_RUN;
+    c.i0 = i0;
+    c.i1 = i1;
+    c.flags = flags;
+    return nmc_call_family(x, c);
+  };
+  int rc = [&]() -> int {
     const int chunk =
         x->launch_iters > 0 && x->launch_iters < x->d.vcap ? x->launch_iters : x->d.vcap;
     for (int c0 = iter_begin; c0 < iter_end; c0 += chunk) {
@@ -611,19 +464,19 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);
       HIPCHK(hipGetLastError());
       if (!partial) {
-        if (int rc = launch_run(x, fam, c0, c1, 0)) return rc;
+        if (int rc = launch_run(c0, c1, 0)) return rc;
       } else if (x->persistent) {
         HIPCHK(hipMemsetAsync(x->d.cnt, 0, (size_t)32 * 8 * x->d.CB * x->P * sizeof(unsigned),
                               x->stream));
-        if (int rc = launch_run(x, fam, c0, c1, NMC_RUN_HYPER_LOAD)) return rc;
+        if (int rc = launch_run(c0, c1, NMC_RUN_HYPER_LOAD)) return rc;
       } else {
         for (int it = c0; it < c1; ++it)
-          if (int rc = launch_run(x, fam, it, it + 1, it == c0 ? NMC_RUN_HYPER_LOAD : 0)) return rc;
+          if (int rc = launch_run(it, it + 1, it == c0 ? NMC_RUN_HYPER_LOAD : 0)) return rc;
         if (int rc = launch_hyper(x, c1 - 1)) return rc;   // closes the chunk
       }
     }
     return 0;
-  });
+  }();
   x->cur_slot = (iter_end - 1) & 1;
   return rc;
 }
@@ -662,14 +515,11 @@ int nmc_eval_group_ll(nmc_ctx* x, const double* theta, double* out) {
   HIPCHK(hipMalloc(&th, PGC * 8));
   HIPCHK(hipMalloc(&o, GC * 8));
   HIPCHK(hipMemcpyAsync(th, theta, PGC * 8, hipMemcpyHostToDevice, x->stream));
-  int rc = with_family(x, [&](auto fam) -> int {
-    using F = decltype(fam);
-    const size_t lds = (size_t)x->d.W * 64 * F::NACC * sizeof(double);
-    hipLaunchKernelGGL(nmc_k_group_ll<F>, dim3(x->d.CB * x->G), dim3(64 * x->d.W), lds,
-                       x->stream, x->d, fam, x->d.obs, (const double*)th, o);
-    HIPCHK(hipGetLastError());
-    return 0;
-  });
+  NmcCall c;
+  c.op = NMC_OP_GROUP_LL;
+  c.in = th;
+  c.out = o;
+  int rc = nmc_call_family(x, c);
   if (!rc) {
     hipError_t e = hipMemcpyAsync(out, o, GC * 8, hipMemcpyDeviceToHost, x->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(x->stream);
@@ -685,18 +535,17 @@ int nmc_eval_obs_ll(nmc_ctx* x, double* out) {
   const size_t n = (size_t)x->C * x->n_obs;
   double* o = nullptr;
   HIPCHK(hipMalloc(&o, (n ? n : 1) * 8));
-  int rc = with_family(x, [&](auto fam) -> int {
-    using F = decltype(fam);
-    hipLaunchKernelGGL(nmc_k_obs_ll<F>, dim3(x->d.CB * x->G), dim3(64), 0, x->stream, x->d,
-                       fam, (const double*)vslot(x, x->cur_slot), o, x->n_obs);
-    HIPCHK(hipGetLastError());
-    return 0;
-  });
+  NmcCall c;
+  c.op = NMC_OP_OBS_LL;
+  c.in = vslot(x, x->cur_slot);
+  c.out = o;
+  int rc = nmc_call_family(x, c);
   if (!rc && n) {
     hipError_t e = hipMemcpyAsync(out, o, n * 8, hipMemcpyDeviceToHost, x->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(x->stream);
     if (e != hipSuccess) rc = fail(-2, std::string("eval_obs_ll: ") + hipGetErrorString(e));
   }
+  if (!rc) rc = check_timeout(x);   // rows from a timed-out persistent launch are not valid
   hipFree(o);
   return rc;
 }
@@ -850,13 +699,24 @@ int nmc_comm_destroy(void* comm) {
   return 0;
 }
 
-int nmc_gather_samples(nmc_ctx* x, void* comm, int root, double* host_out) {
+int nmc_comm_size(void* comm, int* nranks, int* rank) {
+  ncclComm_t c = (ncclComm_t)comm;
+  ncclResult_t r = ncclCommCount(c, nranks);
+  if (r == ncclSuccess) r = ncclCommUserRank(c, rank);
+  if (r != ncclSuccess) return fail(-4, std::string("ncclCommCount: ") + ncclGetErrorString(r));
+  return 0;
+}
+
+int nmc_gather_samples(nmc_ctx* x, void* comm, int root, double* host_out,
+                       int64_t host_capacity) {
   hipSetDevice(x->device);
   ncclComm_t c = (ncclComm_t)comm;
   int nranks = 0, rank = 0;
-  ncclCommCount(c, &nranks);
-  ncclCommUserRank(c, &rank);
+  if (int rc = nmc_comm_size(comm, &nranks, &rank)) return rc;
   const size_t count = (size_t)x->d.n_rows * x->d.cols * x->C;
+  if (rank == root && (!host_out || host_capacity < (int64_t)(count * nranks)))
+    return fail(-1, "gather: the root's host buffer holds fewer than nranks * rows * cols * C "
+                    "doubles");
   double* recv = nullptr;
   if (rank == root) HIPCHK(hipMalloc(&recv, (count ? count : 1) * nranks * 8));
   ncclResult_t r = ncclGather(x->d.samples, recv, count, ncclDouble, root, c, x->stream);

@@ -73,7 +73,8 @@ SIGNATURES = {
     "nmc_comm_init": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_ubyte),
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "nmc_comm_destroy": (ctypes.c_int, [_vp]),
-    "nmc_gather_samples": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _c_double_p]),
+    "nmc_comm_size": (ctypes.c_int, [_vp, _c_int_p, _c_int_p]),
+    "nmc_gather_samples": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _c_double_p, ctypes.c_int64]),
     "nmc_debug_prior_logpdf": (ctypes.c_int, [ctypes.c_int, _c_double_p, _c_double_p,
                                               ctypes.c_int, _c_double_p]),
     "nmc_debug_igamci": (ctypes.c_int, [_c_double_p, _c_double_p, _c_double_p, ctypes.c_int,

@@ -63,15 +63,26 @@ def rccl_destroy(comm):
     _lib.load().nmc_comm_destroy(comm)
 
 
-def gather_samples(engine, comm, root=0, world=None):
-    """ncclGather of every rank's [rows][cols][C_local] store; root gets [rank][...]."""
-    lib = _lib.load()
-    nranks = ctypes.c_int()
-    if world is None:
-        world = 1
-    out = numpy.empty((world, engine.n_rows, engine.cols, engine.C)) if world else None
-    check(lib.nmc_gather_samples(engine.h, comm, root, dptr(out)))
-    return out
+def comm_size(comm):
+    """(nranks, rank) of an RCCL communicator."""
+    n, r = ctypes.c_int(), ctypes.c_int()
+    check(_lib.load().nmc_comm_size(comm, ctypes.byref(n), ctypes.byref(r)))
+    return n.value, r.value
+
+
+def gather_samples(engine, comm, root=0):
+    """ncclGather of every rank's [rows][cols][C_local] store.
+
+    The root gets [rank][rows][cols][C_local]; the other ranks get None (and
+    allocate nothing).  Every rank must hold the same C_local (padded_shard).
+    """
+    world, rank = comm_size(comm)
+    if rank == root:
+        out = numpy.empty((world, engine.n_rows, engine.cols, engine.C))
+        check(_lib.load().nmc_gather_samples(engine.h, comm, root, dptr(out), out.size))
+        return out
+    check(_lib.load().nmc_gather_samples(engine.h, comm, root, None, 0))
+    return None
 
 
 def assemble(gathered, n_real):

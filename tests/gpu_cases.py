@@ -72,3 +72,71 @@ def synthetic(kind, C, G, N, seed=3, ragged=False):
 
 def golden(name):
     return Case(name)
+
+
+def partial_state(fam, sizes, C, P, seed=11, spread=1.0):
+    """A random partial-pooling start ([C] chains) and the oracle's Nested for it."""
+    from oracle import restatement as rs
+    r = numpy.random.RandomState(seed)
+    nested = rs.Nested(fam, sizes)
+    G = len(sizes)
+    mu = r.normal(0, 0.5, size=(C, P)) + numpy.arange(P) * (1.0 if P <= 2 else 0.0)
+    s2 = r.uniform(0.2, 1.0, size=(C, P)) * spread
+    value = mu[:, :, None] + numpy.sqrt(s2)[:, :, None] * r.normal(size=(C, P, G))
+    lp = rs.norm_logpdf(value, mu[:, :, None], numpy.sqrt(s2)[:, :, None])
+    ll = numpy.array([nested.group_ll(value[c]) for c in range(C)])
+    return rs.State(value, lp, ll, mu, s2), nested
+
+
+def run_engine(fam, sizes, st, sel, chain_base, n_iter, seed, pooling="partial", priors=None,
+               env=None, burn=None, thin=1, tune_interval=5, launch_iters=0):
+    """Run the HIP engine on chains ``sel`` of state ``st``; returns
+    (accept flags [C, iter, P, G], proposal LLs, recorded rows [C, rows, cols], launch config)."""
+    import os
+    from nestmc.engine import Engine
+    old = {}
+    for k, v in (env or {}).items():
+        old[k] = os.environ.get(k)
+        os.environ[k] = v
+    try:
+        eng = Engine(fam, sizes, len(sel), pooling, priors, seed=seed, chain_base=chain_base)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
+    mu = None if st.mu is None else st.mu[sel]
+    s2 = None if st.s2 is None else st.s2[sel]
+    eng.set_state(st.value[sel], st.lp[sel], st.ll[sel], mu, s2)
+    eng.set_schedule(n_iter, n_iter // 2 if burn is None else burn, thin,
+                     tune_interval=tune_interval)
+    eng.set_trace(True)
+    if launch_iters:
+        eng.set_launch_iters(launch_iters)
+    eng.run(0, n_iter)
+    acc, llp = eng.trace(n_iter)
+    rows = eng.samples()
+    cfg = eng.launch_config()
+    eng.close()
+    return acc, llp, rows, cfg
+
+
+def run_oracle(nested, st, sel, chain_ids, n_iter, seed, pooling="partial", priors=None,
+               burn=None, thin=1, tune_interval=5):
+    """The numpy oracle on the same Philox stream for chains ``sel`` (global ids chain_ids)."""
+    from oracle import restatement as rs
+    C = len(sel)
+    o = rs.State(st.value[sel].copy(), st.lp[sel].copy(), st.ll[sel].copy(),
+                 None if st.mu is None else st.mu[sel].copy(),
+                 None if st.s2 is None else st.s2[sel].copy())
+    P, G = o.value.shape[1], o.value.shape[2]
+    trace, rec = {}, []
+    rs.run(nested, o, pooling, priors, n_iter, n_iter // 2 if burn is None else burn, thin,
+           rs.PhiloxRNG(numpy.asarray(chain_ids), seed), tune_interval=tune_interval,
+           trace=trace, record=rec)
+    acc = numpy.stack(trace["acc"], 1).reshape(C, n_iter, P, G)
+    llp = numpy.stack(trace["llp"], 1).reshape(C, n_iter, P, G)
+    margin = numpy.min(numpy.stack(trace["margin"]))
+    rows = numpy.stack([r for _, r in rec], 1)
+    return acc, llp, rows, margin

@@ -31,3 +31,27 @@ def test_sample_posterior_writes_reference_csvs(gpu_lib, name, tmp_path):
     for ch in range(c.n_chains):
         mine = os.path.join(out, "sample", "sample.%i.csv" % ch)
         assert filecmp.cmp(mine, c.csv_path(ch), shallow=False), (name, ch)
+
+
+def test_save_loglikelihood_matches_reference(gpu_lib, tmp_path):
+    """saveLogLikelihood=True (the reference's default, posteriorSampling.py:28-35):
+    logLikelihood.<chain>.csv rows (:890-891, :907-909, :656-659) must be the
+    reference's bytes -- sha256 of the whole 1000-row file captured by
+    tests/golden/make_golden.py, plus its first and last rows."""
+    import hashlib
+    c = Case("regression_complete")
+    a = c.arr
+    m = c.meta
+    out = str(tmp_path) + "/"
+    sample_posterior(c.n_chains, c.n_iter, c.n_samples, c.names, c.n_groups, c.n_per_group,
+                     c.pooling, family_for(c), out, saveLogLikelihood=True,
+                     priorDistribution=c.priors, startWithMLE=c.mle,
+                     startingPointValueRange=c.ranges, displayProgress=False,
+                     rng="replay", replay={k: a[k] for k in ("z", "u", "hz", "hu")})
+    raw = open(os.path.join(out, "sample", "logLikelihood.0.csv"), "rb").read()
+    lines = raw.decode().splitlines()
+    assert len(lines) == m["ll0_rows"]
+    assert lines[0] == m["ll0_first"]
+    assert lines[-1] == m["ll0_last"]
+    assert hashlib.sha256(raw).hexdigest() == m["ll0_sha256"]
+    assert filecmp.cmp(os.path.join(out, "sample", "sample.0.csv"), c.csv_path(0), shallow=False)

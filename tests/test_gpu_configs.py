@@ -1,0 +1,155 @@
+"""GPU parity on the geometry of BASELINE configs 4 and 5 and the kernel branches
+they take (SURVEY 8(d) cfg 4/5), against the numpy oracle on the same Philox stream.
+
+* cfg-4 shard geometry: G = 129 / 256 groups of 2000 rows -> more than one numpy
+  pairwise leaf in the Gibbs update (posteriorSampling.py:481-498), persistent
+  (one chain block, 256 workgroups) and launch-per-iteration (two chain blocks);
+  all chains must agree bit for bit across launch modes and chain-block counts.
+* cfg-5 shape: 8-parameter logistic, 5000 rows per group (rows exceed the 64 KiB
+  LDS tile -> rows streamed from global memory, :615-635), P > 2 closing update.
+* odd chain counts in the payload-in-LDS Gibbs mode (register fallback).
+* launch-per-iteration grids larger than one residency wave.
+* one-rank RCCL gather of the sample store.
+Tolerances: accept flags bit-exact; values and proposal LLs within 1e-9 relative.
+"""
+
+import ctypes
+
+import numpy
+import pytest
+
+from gpu_cases import partial_state, run_engine, run_oracle
+from nestmc import data
+from nestmc.families import LinearRegression, Logistic
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, rtol=1e-9):
+    return numpy.allclose(a, b, rtol=rtol, atol=1e-9, equal_nan=True)
+
+
+def _check_vs_oracle(dev, nested, st, sel, chain_ids, n_iter, seed, **kw):
+    acc, llp, rows, _ = dev
+    oacc, ollp, orows, margin = run_oracle(nested, st, sel, chain_ids, n_iter, seed, **kw)
+    bad = numpy.argwhere(acc[sel].astype(bool) != oacc)
+    assert bad.size == 0, "flag mismatch at %s (min margin %g)" % (bad[:5], margin)
+    assert _close(llp[sel], ollp, rtol=1e-10)
+    assert _close(rows[sel], orows)
+
+
+@pytest.mark.parametrize("G", [129, 256])
+def test_cfg4_geometry_multileaf_gibbs(gpu_lib, G):
+    N, n_iter, seed = 2000, 8, 31
+    x, y, _, _ = data.linreg(G, N, seed=7)
+    fam = LinearRegression.simple(x, y, sigma=1.0)
+    sizes = [N] * G
+    C = 128
+    st, nested = partial_state(fam, sizes, C, 2)
+    # one chain block: G workgroups, co-resident -> persistent (SYNC, multi-leaf plan)
+    one = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed)
+    assert one[3]["persistent"], one[3]
+    # the same chains in a two-block launch (launch per iteration at G = 256) and forced
+    # launch per iteration
+    two = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed)
+    lau = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, env={"NMC_PERSIST": "0"})
+    assert not lau[3]["persistent"]
+    for k in range(3):
+        assert numpy.array_equal(one[k], two[k][:64], equal_nan=True), k
+        assert numpy.array_equal(two[k], lau[k], equal_nan=True), k
+    assert 0.05 < lau[0].mean() < 0.95
+    # chains 0, 1 and 127 against the oracle
+    sel = numpy.array([0, 1, 127])
+    _check_vs_oracle(lau, nested, st, sel, sel, n_iter, seed)
+
+
+def test_cfg5_logistic_p8_rows_beyond_lds(gpu_lib):
+    G, N, n_iter, seed = 6, 5000, 5, 5
+    X, yl, _ = data.logistic(G, N, n_coef=8, seed=1)
+    fam = Logistic(X, yl)
+    assert fam.n_params == 8 and fam.n_fields == 8 and N * 8 * 8 > 64 * 1024
+    sizes = [N] * G
+    C = 64
+    st, nested = partial_state(fam, sizes, C, 8, spread=0.1)
+    dev = run_engine(fam, sizes, st, numpy.arange(C), 100, n_iter, seed, tune_interval=2)
+    assert dev[3]["persistent"]
+    lau = run_engine(fam, sizes, st, numpy.arange(C), 100, n_iter, seed, tune_interval=2,
+                     env={"NMC_PERSIST": "0"})
+    for k in range(3):
+        assert numpy.array_equal(dev[k], lau[k], equal_nan=True), k
+    sel = numpy.array([0, 63])
+    _check_vs_oracle(dev, nested, st, sel, sel + 100, n_iter, seed, tune_interval=2)
+    assert dev[0].mean() > 0.02
+
+
+@pytest.mark.parametrize("C", [65, 63])
+def test_odd_chain_count_payload_in_lds(gpu_lib, C):
+    G, N, n_iter, seed = 40, 256, 10, 77
+    x, y, _, _ = data.linreg(G, N, seed=3)
+    fam = LinearRegression.simple(x, y, sigma=1.0)
+    sizes = [N] * G
+    st, nested = partial_state(fam, sizes, C, 2)
+    dev = run_engine(fam, sizes, st, numpy.arange(C), 9, n_iter, seed)
+    assert dev[3]["persistent"] and dev[3]["waves_per_group"] >= 4
+    sel = numpy.arange(C)
+    _check_vs_oracle(dev, nested, st, sel, sel + 9, n_iter, seed)
+
+
+def test_launch_mode_grid_beyond_residency(gpu_lib):
+    """4096 chains x 64 groups launched per iteration (4096 workgroups, more than the
+    chip holds at once): every chain block must read the hyper-parameters of the
+    previous iteration, whatever dispatch wave its workgroups land in."""
+    G, N, n_iter, seed = 64, 64, 8, 12
+    x, y, _, _ = data.linreg(G, N, seed=5)
+    fam = LinearRegression.simple(x, y, sigma=1.0)
+    sizes = [N] * G
+    C = 4096
+    st, nested = partial_state(fam, sizes, C, 2)
+    big = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, env={"NMC_PERSIST": "0"})
+    assert not big[3]["persistent"]
+    for lo in (0, C - 64):
+        sel = numpy.arange(lo, lo + 64)
+        small = run_engine(fam, sizes, st, sel, lo, n_iter, seed)
+        for k in range(3):
+            assert numpy.array_equal(big[k][sel], small[k], equal_nan=True), (lo, k)
+    sel = numpy.array([0, 2047, 4095])
+    _check_vs_oracle(big, nested, st, sel, sel, n_iter, seed)
+
+
+def test_rccl_gather_one_rank(gpu_lib):
+    from nestmc import parallel
+    from nestmc.engine import Engine
+    G, N, C, n_iter = 8, 50, 70, 12
+    x, y, _, _ = data.linreg(G, N, seed=2)
+    fam = LinearRegression.simple(x, y, sigma=1.0)
+    sizes = [N] * G
+    st, _ = partial_state(fam, sizes, C, 2)
+    eng = Engine(fam, sizes, C, "partial", seed=3)
+    eng.set_state(st.value, st.lp, st.ll, st.mu, st.s2)
+    eng.set_schedule(n_iter, 4, 2)
+    eng.run(0, n_iter)
+    want = eng.samples_raw()
+    comm = parallel.rccl_comm(None, 1, 0, 0)
+    try:
+        assert parallel.comm_size(comm) == (1, 0)
+        got = parallel.gather_samples(eng, comm, root=0)
+    finally:
+        parallel.rccl_destroy(comm)
+    eng.close()
+    assert got.shape == (1,) + want.shape
+    assert numpy.array_equal(got[0], want)
+    # a root buffer that is too small is refused, not overrun
+    from nestmc import _lib
+    comm = parallel.rccl_comm(None, 1, 0, 0)
+    try:
+        eng = Engine(fam, sizes, C, "partial", seed=3)
+        eng.set_state(st.value, st.lp, st.ll, st.mu, st.s2)
+        eng.set_schedule(n_iter, 4, 2)
+        small = numpy.empty(10)
+        rc = _lib.load().nmc_gather_samples(eng.h, comm, 0,
+                                            small.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                            small.size)
+        assert rc != 0
+        eng.close()
+    finally:
+        parallel.rccl_destroy(comm)
