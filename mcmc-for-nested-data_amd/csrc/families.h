@@ -34,6 +34,7 @@ struct FamLinreg {
   static constexpr int MAXP = NF + 1;   // parameters a row of NF fields can involve
   static constexpr int NACC = 1;
   static constexpr int K = NF - 1;
+  static constexpr bool ASM_ROWS = NF == 2;   // {x, y} rows: hand-written LDS row loop
   int intercept;
   double sigma_known;   // > 0: fixed noise sd; else sigma is the last parameter
   double log_sigma_known;
@@ -111,6 +112,7 @@ struct FamLinreg {
 template <int NF>
 struct FamGaussMean {
   static constexpr int NFIELDS = NF;
+  static constexpr bool ASM_ROWS = false;
   static constexpr int MAXP = NF + 1;   // parameters a row of NF fields can involve
   static constexpr int NACC = NF;
   double sd[NF];
@@ -185,6 +187,7 @@ struct FamGaussMean {
 template <int NF>
 struct FamLogistic {
   static constexpr int NFIELDS = NF;
+  static constexpr bool ASM_ROWS = false;
   static constexpr int MAXP = NF + 1;   // parameters a row of NF fields can involve
   static constexpr int NACC = 1;
   static constexpr int K = NF - 1;

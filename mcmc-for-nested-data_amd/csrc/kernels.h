@@ -72,6 +72,7 @@ struct Dev {
   int hlds, naux;        // persistent partial: Gibbs payload via LDS, auxiliary waves
   int noprio;            // diagnostics: no issue priority for the latency-bound waves
   int rows_lds;          // 1: each workgroup stages its group's rows in LDS once per launch
+  int tile;              // target rows per likelihood tile (nmc_tiles)
   unsigned* cnt;         // [CB][P][32] publish counters (persistent partial), zeroed per launch
   unsigned* tmo;         // timeout word (persists; host checks it)
   // variates of iterations [vbase, vbase + vcap): filled by nmc_k_fill
@@ -171,12 +172,12 @@ struct nmc_lds_layout {
   int part;    // [NACC][16]     per-wave likelihood partial sums (unused slots: -0.0)
   int st;      // [5][P]         scale, log prior, n acc, n rej, total acc (control wave)
   int hyp;     // [6][P]         mu, sd, log sd, sigma2, sqrt(sigma2/G), 1/sd of the hyper-prior
-  int hval;    // [2][G + 1]     Gibbs payload of one task, two buffers (payload-in-LDS mode)
+  int hval;    // [2][G + 1]     Gibbs payload of two tasks (persistent Gibbs-wave mode)
   int hst;     // [P][nleaf][8 + ntail]  stream sums / tail elements (pairwise sum)
   int hleaf;   // [P][nleaf]     leaf sums
   int zl;      // [2][2]         {z, log u} of this and the next step (LDS-DMA, step parity)
   int hv;      // [2P]           {hyper z, gamma} of the Gibbs update (LDS-DMA)
-  int cw;      // [15]           control-wave temporaries across the step barrier
+  int cw;      // [16]           control-wave values across the step barriers
   int flag;    // [1]            broadcast / epoch words
   int xchg;    // [2][8]         stream sums exchanged by the two compute waves
   int rows;    // [nrows_lds][NF] the group's observation rows (staged once per launch)
@@ -191,24 +192,23 @@ __host__ __device__ inline nmc_lds_layout nmc_lds(int nacc, int P, int partial, 
   L.st = L.part + nacc * 16;   // 16 partial slots per accumulator (unused: -0.0)
   L.hyp = L.st + 5 * P;
   L.hval = L.hyp + (partial ? 6 * P : 0);
-  L.hst = L.hval + (partial && hlds ? 2 * (G + 1) : 0);   // two task buffers, each + 1 DMA pad
+  L.hst = L.hval + (partial && hlds ? 2 * (G + 1) : 0);   // two payload buffers (+1 DMA pad)
   L.hleaf = L.hst + (partial ? P * nleaf * (8 + ntail) : 0);
   L.zl = L.hleaf + (partial ? P * nleaf : 0);
   L.hv = L.zl + 4;
   L.cw = L.hv + (partial ? 2 * P : 0);
-  L.flag = L.cw + 15;
+  L.flag = L.cw + 16;
   L.xchg = L.flag + 1;
-  L.rows = L.xchg + (partial && hlds ? 16 : 0);
-  L.total = L.rows + (row_doubles + 63) / 64;
+  L.rows = L.xchg;
+  // (+1 column: the pipelined likelihood loop prefetches one block past a wave's rows)
+  L.total = L.rows + (row_doubles > 0 ? (row_doubles + 63) / 64 + 1 : 0);
   return L;
 }
 enum { NMC_ST_S = 0, NMC_ST_LP, NMC_ST_NA, NMC_ST_NR, NMC_ST_TA };
 enum { NMC_HY_MU = 0, NMC_HY_SD, NMC_HY_LSD, NMC_HY_S2, NMC_HY_SDM, NMC_HY_ISD };
-// (PAC, PLP, PLL: the decided step's accept flag, log prior and log-likelihood, applied
-// to the state by the control wave at the next step, off the critical path)
-enum { NMC_CW_LU = 0, NMC_CW_LPC, NMC_CW_LPP, NMC_CW_PROP, NMC_CW_SA, NMC_CW_SR, NMC_CW_NAA,
-       NMC_CW_NRA, NMC_CW_NAR, NMC_CW_NRR, NMC_CW_TA, NMC_CW_V, NMC_CW_PAC, NMC_CW_PLP,
-       NMC_CW_PLL };
+// control-wave columns of the LDS carve (cw): LPC/LPP: priors of the step made by the
+// Gibbs wave; NAA..TA: counter outcomes of the decided step
+enum { NMC_CW_LPC = 0, NMC_CW_LPP, NMC_CW_NAA, NMC_CW_NRA, NMC_CW_NAR, NMC_CW_NRR, NMC_CW_TA };
 
 // Where the Gibbs update reads the published values: global (plain loads after a
 // kernel boundary / sc1 loads in a persistent launch) or the LDS copy the
@@ -391,200 +391,6 @@ __device__ __forceinline__ void nmc_hyper(const Dev& d, const double* src, int c
   __syncthreads();
 }
 
-// ONE wave computes the Gibbs update of parameter p after iteration t for its 64
-// chains (persistent payload-in-LDS mode, run by an auxiliary wave during the step-0
-// likelihood): the chain block's published values of p (sc1 loads) are staged in
-// LDS hval[p], then numpy's pairwise sums give mean and variance (G <= 128: one
-// numpy leaf; the host enables this mode only then).
-// hz/hx: this lane's hyper variates of (t, p).  Writes the LDS hyp columns of p.
-// numpy's pairwise sum of one leaf (n <= 128 values v[i * 64], optionally squared
-// deviations from mu): r_j = x_j + x_{j+8} + ..., ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)),
-// then the n % 8 tail in order; n < 8: a plain sequential sum from 0.
-template <bool SQ>
-__device__ __forceinline__ double nmc_leaf_sum(const double* v, int n, double mu) {
-  auto f = [&](int i) -> double {
-    double x = v[i * 64];
-    if (SQ) {
-      x = x - mu;
-      x = x * x;
-    }
-    return x;
-  };
-  const int m8 = n >= 8 ? n - n % 8 : 0;
-  double res = 0.0;
-  if (m8) {
-    double r[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = f(j);
-    for (int i = 8; i < m8; i += 8) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = r[j] + f(i + j);
-    }
-    res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  }
-  for (int i = m8; i < n; ++i) res += f(i);
-  return res;
-}
-
-// Groups [kb, ke) of the chain block's published values of parameter p (64 chains
-// each) -> LDS hval, sc1 loads, 8 in flight (used when C is odd).
-__device__ __forceinline__ void nmc_hyper_load(const Dev& d, const double* src, int p, int cc,
-                                               int kb, int ke, double* lds,
-                                               const nmc_lds_layout& L, int hoff) {
-  const int lane = threadIdx.x & 63;
-  const int C = d.C;
-  src += (size_t)p * d.G * C;
-  constexpr int NB = 8;   // the odd-C fallback of the LDS-DMA copy: few registers
-  for (int k0 = kb; k0 < ke; k0 += NB) {
-    double tv[NB];
-#pragma unroll
-    for (int u = 0; u < NB; ++u)
-      tv[u] = k0 + u < ke ? nmc_ldv<NMC_SRC_SC1>(src + (size_t)(k0 + u) * C + cc) : 0.0;
-#pragma unroll
-    for (int u = 0; u < NB; ++u)
-      if (k0 + u < ke) lds[(size_t)(L.hval + hoff + k0 + u) * 64 + lane] = tv[u];
-  }
-}
-
-// The same by LDS-DMA (global_load_lds_dwordx4, sc1): one instruction moves two groups'
-// 64-chain rows (lanes 0-31 / 32-63, two chains per lane) into two consecutive hval
-// columns, so one wave has the whole payload in flight without registers.  Needs C
-// even (16-byte rows); an odd group count writes one pad column past ke.  The issuing
-// wave retires the copies with s_waitcnt vmcnt(0).
-__device__ __forceinline__ void nmc_hyper_dma(const Dev& d, const double* src, int p, int cb,
-                                              int kb, int ke, double* lds,
-                                              const nmc_lds_layout& L, int hoff) {
-  const int lane = threadIdx.x & 63;
-  const double* s = src + (size_t)p * d.G * d.C + (size_t)cb * 64 + 2 * (lane & 31);
-  for (int k0 = kb; k0 < ke; k0 += 2) {
-    const int gk = k0 + (lane >> 5) < ke ? k0 + (lane >> 5) : ke - 1;
-    __builtin_amdgcn_global_load_lds((nmc_glb_ptr)(s + (size_t)gk * d.C),
-                                     (nmc_lds_ptr)(lds + (size_t)(L.hval + hoff + k0) * 64), 16,
-                                     0, 16 /* sc1 */);
-  }
-}
-
-// The Gibbs update of parameter p after iteration t for this wave's 64 chains from
-// the LDS copy hval of p's values (G <= 128: one numpy leaf).  hz/hx: this lane's hyper
-// variates of (t, p).  Writes the LDS hyp columns of p (and, if write, global + row).
-__device__ __forceinline__ void nmc_hyper_compute(const Dev& d, int cb, int t, int p, double* lds,
-                                                  const nmc_lds_layout& L, bool write, double hz,
-                                                  double hx, int hoff) {
-  const int lane = threadIdx.x & 63;
-  const int P = d.P, G = d.G, C = d.C;
-  const int c = cb * 64 + lane;
-  const double* hv = lds + (size_t)(L.hval + hoff) * 64 + lane;   // hv[i * 64]: group i of p
-  double* hy = lds + L.hyp * 64 + lane;
-  const double sdm = sqrt(hy[(NMC_HY_S2 * P + p) * 64] / G);
-  const double tot = nmc_leaf_sum<false>(hv, G, 0.0);
-  const double mu = tot / G + sdm * hz;                        // mu ~ N(mean(x), sqrt(s2/G))
-  const double ss = nmc_leaf_sum<true>(hv, G, mu);
-  const double hat = ss / (double)(G - 1);
-  const double scale = d.ha * hat;
-  // scipy invgamma.rvs: (1/gammainccinv(a, U)) * scale + loc; loc when scale == 0
-  const double s2n = scale == 0.0 ? 0.0 : (1.0 / hx) * scale;
-  const double sdn = sqrt(s2n);
-  const double lsd = log(sdn);
-  hy[(NMC_HY_MU * P + p) * 64] = mu;
-  hy[(NMC_HY_SD * P + p) * 64] = sdn;
-  hy[(NMC_HY_LSD * P + p) * 64] = lsd;
-  hy[(NMC_HY_S2 * P + p) * 64] = s2n;
-  hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
-  if (write && c < C) {
-    const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
-    d.mu[ho] = mu;
-    d.s2[ho] = s2n;
-    d.hsd[ho] = sdn;
-    d.hlsd[ho] = lsd;
-    const int row = nmc_record_row(d, t);
-    if (row >= 0) {
-      double* out = d.samples + ((size_t)row * d.cols + (size_t)p * (G + 2)) * C + c;
-      out[0] = mu;
-      out[C] = s2n;
-    }
-  }
-}
-
-// The same update split over two waves (half 0 / 1 sum numpy streams 0-3 / 4-7 of both
-// leaf sums and swap the stream sums through LDS, so both combine all eight in numpy's
-// order); half 0 finishes and writes.  epoch: unique per task, > every earlier one.
-// Both waves must call it (bounded spins).  Needs G >= 8.
-__device__ __forceinline__ void nmc_hyper_compute2(const Dev& d, int cb, int t, int p, double* lds,
-                                                   const nmc_lds_layout& L, bool write, double hz,
-                                                   double hx, int hoff, int half, double epoch) {
-  const int lane = threadIdx.x & 63;
-  const int P = d.P, G = d.G, C = d.C;
-  const int c = cb * 64 + lane;
-  const double* hv = lds + (size_t)(L.hval + hoff) * 64 + lane;
-  double* hy = lds + L.hyp * 64 + lane;
-  double* xc = lds + (size_t)L.xchg * 64 + lane;
-  double* fl = lds + L.flag * 64 + 16;
-  const double sdm = sqrt(hy[(NMC_HY_S2 * P + p) * 64] / G);
-  const int m8 = G - G % 8;
-  auto leaf = [&](int st, bool sq, double mu) -> double {
-    auto f = [&](int i) -> double {
-      double x = hv[i * 64];
-      if (sq) {
-        x = x - mu;
-        x = x * x;
-      }
-      return x;
-    };
-    double r[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) r[jj] = f(4 * half + jj);
-    for (int i = 8; i < m8; i += 8) {
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) r[jj] = r[jj] + f(i + 4 * half + jj);
-    }
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) xc[(st * 8 + 4 * half + jj) * 64] = r[jj];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0)
-      __hip_atomic_store(fl + st * 2 + half, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    for (unsigned spins = 0;
-         __hip_atomic_load(fl + st * 2 + (1 - half), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) !=
-             epoch &&
-         spins < NMC_SPIN_LIMIT;
-         ++spins)
-      __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double rr[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) rr[j] = xc[(st * 8 + j) * 64];
-    double res = ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
-    for (int i = m8; i < G; ++i) res += f(i);
-    return res;
-  };
-  const double tot = leaf(0, false, 0.0);
-  const double mu = tot / G + sdm * hz;
-  const double ss = leaf(1, true, mu);
-  if (half != 0) return;
-  const double hat = ss / (double)(G - 1);
-  const double scale = d.ha * hat;
-  const double s2n = scale == 0.0 ? 0.0 : (1.0 / hx) * scale;
-  const double sdn = sqrt(s2n);
-  const double lsd = log(sdn);
-  hy[(NMC_HY_MU * P + p) * 64] = mu;
-  hy[(NMC_HY_SD * P + p) * 64] = sdn;
-  hy[(NMC_HY_LSD * P + p) * 64] = lsd;
-  hy[(NMC_HY_S2 * P + p) * 64] = s2n;
-  hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
-  if (write && c < C) {
-    const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
-    d.mu[ho] = mu;
-    d.s2[ho] = s2n;
-    d.hsd[ho] = sdn;
-    d.hlsd[ho] = lsd;
-    const int row = nmc_record_row(d, t);
-    if (row >= 0) {
-      double* out = d.samples + ((size_t)row * d.cols + (size_t)p * (G + 2)) * C + c;
-      out[0] = mu;
-      out[C] = s2n;
-    }
-  }
-}
-
 // The calling wave polls the chain block's publish counter until it reaches target
 // (bounded; a timeout is recorded in d.tmo and reported by the host).  The counter is
 // sharded 8 ways (workgroup g adds to shard g % 8, each shard on its own 128-B line)
@@ -656,6 +462,69 @@ __device__ __forceinline__ void nmc_ll_rows(const Fam& fam, const typename Fam::
   for (int k = 0; k < Fam::NACC; ++k) acc[k] = (a[0][k] + a[1][k]) + (a[2][k] + a[3][k]);
 }
 
+// The regression row loop (FamLinreg<2>: rows {x, y}, e = fma(x, b1, b0) - y,
+// acc[i & 3] = fma(e, e, acc[i & 3]) for row i of each 8-row block) written by hand:
+// two fixed register sets v[192:223] / v[224:255], block b+1's eight broadcast
+// ds_read_b128 in flight while block b is consumed (counted lgkmcnt(8)).  The compiler
+// does not keep this prefetch (it sinks the reads below the arithmetic and copies the
+// register sets); measured at the LDS-broadcast floor, ~5 cycles per row per CU
+// (tools/llbench4.hip).  Same operations in the same order as FamLinreg::accumN, so
+// the sums are bit-identical to the C++ loop.  nb: even number of 8-row blocks >= 2.
+#define NMC_L8(b, off)                                                     \
+  "ds_read_b128 v[" #b "+0:" #b "+3], %[addr] offset:" #off "+0\n"         \
+  "ds_read_b128 v[" #b "+4:" #b "+7], %[addr] offset:" #off "+16\n"        \
+  "ds_read_b128 v[" #b "+8:" #b "+11], %[addr] offset:" #off "+32\n"       \
+  "ds_read_b128 v[" #b "+12:" #b "+15], %[addr] offset:" #off "+48\n"      \
+  "ds_read_b128 v[" #b "+16:" #b "+19], %[addr] offset:" #off "+64\n"      \
+  "ds_read_b128 v[" #b "+20:" #b "+23], %[addr] offset:" #off "+80\n"      \
+  "ds_read_b128 v[" #b "+24:" #b "+27], %[addr] offset:" #off "+96\n"      \
+  "ds_read_b128 v[" #b "+28:" #b "+31], %[addr] offset:" #off "+112\n"
+#define NMC_E(b, k) \
+  "v_fma_f64 v[" #b "+" #k ":" #b "+" #k "+1], v[" #b "+" #k ":" #b "+" #k "+1], %[b1], %[b0]\n"
+#define NMC_D(b, k)                                                                  \
+  "v_add_f64 v[" #b "+" #k ":" #b "+" #k "+1], v[" #b "+" #k ":" #b "+" #k "+1], -v[" #b \
+  "+" #k "+2:" #b "+" #k "+3]\n"
+#define NMC_S(b, k, a) \
+  "v_fma_f64 %[" #a "], v[" #b "+" #k ":" #b "+" #k "+1], v[" #b "+" #k ":" #b "+" #k "+1], %[" #a "]\n"
+#define NMC_B8(b)                                                                       \
+  NMC_E(b, 0) NMC_E(b, 4) NMC_E(b, 8) NMC_E(b, 12) NMC_E(b, 16) NMC_E(b, 20) NMC_E(b, 24)  \
+  NMC_E(b, 28) NMC_D(b, 0) NMC_D(b, 4) NMC_D(b, 8) NMC_D(b, 12) NMC_D(b, 16) NMC_D(b, 20)  \
+  NMC_D(b, 24) NMC_D(b, 28) NMC_S(b, 0, a0) NMC_S(b, 4, a1) NMC_S(b, 8, a2)               \
+  NMC_S(b, 12, a3) NMC_S(b, 16, a0) NMC_S(b, 20, a1) NMC_S(b, 24, a2) NMC_S(b, 28, a3)
+typedef __attribute__((address_space(3))) const double* nmc_lds_cptr;
+__device__ __forceinline__ void nmc_rows_lds_linreg2(const double* p, int nb, double b0,
+                                                     double b1, double& a0, double& a1,
+                                                     double& a2, double& a3) {
+  unsigned addr = (unsigned)(uintptr_t)(nmc_lds_cptr)p;
+  int cnt = nb;
+  asm volatile(
+      NMC_L8(192, 0)
+      "L_nmc_rows_%=:\n"
+      NMC_L8(224, 128)
+      "s_waitcnt lgkmcnt(8)\n"
+      NMC_B8(192)
+      "v_add_u32 %[addr], 0x100, %[addr]\n"
+      "s_sub_u32 %[cnt], %[cnt], 2\n"
+      "s_cmp_gt_i32 %[cnt], 0\n"
+      "s_cbranch_scc0 L_nmc_last_%=\n"
+      NMC_L8(192, 0)
+      "s_waitcnt lgkmcnt(8)\n"
+      NMC_B8(224)
+      "s_branch L_nmc_rows_%=\n"
+      "L_nmc_last_%=:\n"
+      "s_waitcnt lgkmcnt(0)\n"
+      NMC_B8(224)
+      : [addr] "+v"(addr), [cnt] "+s"(cnt), [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2),
+        [a3] "+v"(a3)
+      : [b0] "v"(b0), [b1] "v"(b1)
+      : "v192", "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200", "v201", "v202",
+        "v203", "v204", "v205", "v206", "v207", "v208", "v209", "v210", "v211", "v212", "v213",
+        "v214", "v215", "v216", "v217", "v218", "v219", "v220", "v221", "v222", "v223", "v224",
+        "v225", "v226", "v227", "v228", "v229", "v230", "v231", "v232", "v233", "v234", "v235",
+        "v236", "v237", "v238", "v239", "v240", "v241", "v242", "v243", "v244", "v245", "v246",
+        "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255", "scc", "memory");
+}
+
 // The same over rows staged in LDS: blocks of R rows read with wave-uniform
 // (broadcast) ds_reads; block b+1 is requested before block b is consumed (LDS
 // returns in order, so the wait covers only block b).
@@ -676,22 +545,49 @@ __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename F
   for (int s = 0; s < 4; ++s)
 #pragma unroll
     for (int k = 0; k < Fam::NACC; ++k) a[s][k] = 0.0;
-  const int nb = n / R;
-  if (nb > 0) {
-    double cur[R * NF];
+  // two register sets A/B over an even number of R-row blocks: block b+1's reads are
+  // issued before block b is consumed, pinned by scheduling barriers (left alone the
+  // compiler sinks the reads below the arithmetic and every block pays the full LDS
+  // latency).  No condition inside the loop (a conditional load costs register
+  // copies): the last prefetch reads one block past the range, which the LDS row
+  // area is padded for (nmc_lds) and which is never consumed.
+  const int nb2 = (n / R) & ~1;
+  if constexpr (Fam::ASM_ROWS) {
+    static_assert(R == 8 && NF == 2, "the asm row loop is the 8-row {x, y} block");
+    if (nb2 > 0) nmc_rows_lds_linreg2(p, nb2, reg.b0, reg.b[0], a[0][0], a[1][0], a[2][0], a[3][0]);
+  } else if (nb2 > 0) {
+    double A[R * NF], B[R * NF];
 #pragma unroll
-    for (int j = 0; j < R * NF; ++j) cur[j] = p[j];
-    for (int b = 0; b < nb; ++b) {
-      const int bn = b + 1 < nb ? b + 1 : b;
-      double nxt[R * NF];
+    for (int j = 0; j < R * NF; ++j) A[j] = p[j];
+    for (int b = 0; b < nb2; b += 2) {
+      const double* q = p + (size_t)b * (R * NF);
 #pragma unroll
-      for (int j = 0; j < R * NF; ++j) nxt[j] = p[(size_t)bn * (R * NF) + j];
-      fam.template accumN<R>(reg, cur, a);
+      for (int j = 0; j < R * NF; ++j) B[j] = q[R * NF + j];
+      __builtin_amdgcn_sched_barrier(0);
+      fam.template accumN<R>(reg, A, a);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int j = 0; j < R * NF; ++j) cur[j] = nxt[j];
+      for (int j = 0; j < R * NF; ++j) A[j] = q[2 * R * NF + j];
+      __builtin_amdgcn_sched_barrier(0);
+      fam.template accumN<R>(reg, B, a);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
-  for (int r = nb * R; r < n; ++r) fam.accum(reg, p + (size_t)r * NF, a[0]);
+  // the remaining (< 2R) rows into a[0], in order; their reads are issued in batches of
+  // TB rows (one LDS round trip per batch, not per row)
+  constexpr int TB = (16 / NF) > 0 ? (16 / NF) : 1;
+  for (int r0 = nb2 * R; r0 < n; r0 += TB) {
+    double tv[TB * NF];
+#pragma unroll
+    for (int i = 0; i < TB; ++i) {
+      const int rr = r0 + i < n ? r0 + i : n - 1;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) tv[i * NF + f] = p[(size_t)rr * NF + f];
+    }
+#pragma unroll
+    for (int i = 0; i < TB; ++i)
+      if (r0 + i < n) fam.accum(reg, tv + i * NF, a[0]);
+  }
 #pragma unroll
   for (int k = 0; k < Fam::NACC; ++k) acc[k] = (a[0][k] + a[1][k]) + (a[2][k] + a[3][k]);
 }
@@ -721,21 +617,170 @@ __device__ __forceinline__ void nmc_load_theta(const Dev& d, const double* src, 
 }
 
 // ---------------------------------------------------------------------------
+// Row tiles of one group (the likelihood partition): NT = min(16, ceil(n/tile)) tiles
+// (tile = 64 rows unless a diagnostics override sets it)
+// of TL rows (a multiple of 16, so every tile but the last runs whole 16-row blocks
+// of the pipelined loop), the last tile taking the rest.  Depends only on the group's
+// row count: the tile partials -- and so every log-likelihood sum -- are the same
+// whichever wave computes a tile, whatever the chain count, launch mode or GPU count.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void nmc_tiles(int n, int tile, int* nt, int* tl) {
+  if (n <= 0) {
+    *nt = 1;
+    *tl = 0;
+    return;
+  }
+  int t = (n + tile - 1) / tile;
+  if (t > 16) t = 16;
+  int per = (n + t - 1) / t;
+  per = (per + 15) & ~15;
+  *tl = per;
+  *nt = (n + per - 1) / per;
+}
+
+// Groups [kb, ke) of the chain block's published values of parameter p (64 chains
+// each) -> LDS hval, sc1 loads, 8 in flight (used when C is odd).
+__device__ __forceinline__ void nmc_hyper_load(const Dev& d, const double* src, int p, int cc,
+                                               int kb, int ke, double* lds,
+                                               const nmc_lds_layout& L, int hoff) {
+  const int lane = threadIdx.x & 63;
+  const int C = d.C;
+  src += (size_t)p * d.G * C;
+  constexpr int NB = 8;   // the odd-C fallback of the LDS-DMA copy: few registers
+  for (int k0 = kb; k0 < ke; k0 += NB) {
+    double tv[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      tv[u] = k0 + u < ke ? nmc_ldv<NMC_SRC_SC1>(src + (size_t)(k0 + u) * C + cc) : 0.0;
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      if (k0 + u < ke) lds[(size_t)(L.hval + hoff + k0 + u) * 64 + lane] = tv[u];
+  }
+}
+
+// The same by LDS-DMA (global_load_lds_dwordx4, sc1): one instruction moves two groups'
+// 64-chain rows (lanes 0-31 / 32-63, two chains per lane) into two consecutive hval
+// columns, so one wave has the whole payload in flight without registers.  Needs C
+// even (16-byte rows); an odd group count writes one pad column past ke.  The issuing
+// wave retires the copies with s_waitcnt vmcnt(0).
+__device__ __forceinline__ void nmc_hyper_dma(const Dev& d, const double* src, int p, int cb,
+                                              int kb, int ke, double* lds,
+                                              const nmc_lds_layout& L, int hoff) {
+  const int lane = threadIdx.x & 63;
+  const double* s = src + (size_t)p * d.G * d.C + (size_t)cb * 64 + 2 * (lane & 31);
+  for (int k0 = kb; k0 < ke; k0 += 2) {
+    const int gk = k0 + (lane >> 5) < ke ? k0 + (lane >> 5) : ke - 1;
+    __builtin_amdgcn_global_load_lds((nmc_glb_ptr)(s + (size_t)gk * d.C),
+                                     (nmc_lds_ptr)(lds + (size_t)(L.hval + hoff + k0) * 64), 16,
+                                     0, 16 /* sc1 */);
+  }
+}
+
+// The Gibbs update of parameter p after iteration t for this wave's 64 chains, by ONE
+// wave, from the LDS copy hval of the chain block's values of p (hv[i * 64]: group i):
+// numpy's pairwise sum (8 interleaved streams r_j = x_j + x_{j+8} + ..., combined
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), the G % 8 tail added in order; G < 8: a
+// sequential sum from 0; G <= 128: one numpy leaf) for mean(x) and sum((x - mu)^2)
+// (HyperParameter._updateMean :481-487, _updateVar :489-498).  Run beside the
+// likelihood tiles: reads in bursts of 4 elements per stream (32 in flight, one LDS
+// round trip per burst under the tiles' broadcast traffic).  hz/hx: this lane's hyper variates of
+// (t, p).  Writes the LDS hyp columns of p (and, if write, the global slot of t and the
+// sample row of t).
+__device__ __forceinline__ void nmc_hyper_compute(const Dev& d, int cb, int t, int p, double* lds,
+                                                  const nmc_lds_layout& L, bool write, double hz,
+                                                  double hx, int hoff) {
+  const int lane = threadIdx.x & 63;
+  const int P = d.P, G = d.G, C = d.C;
+  const int c = cb * 64 + lane;
+  const double* hv = lds + (size_t)(L.hval + hoff) * 64 + lane;   // hv[i * 64]: group i of p
+  double* hy = lds + L.hyp * 64 + lane;
+  const double sdm = sqrt(hy[(NMC_HY_S2 * P + p) * 64] / G);
+  const int m8 = G >= 8 ? G - G % 8 : 0;
+  const int cnt = m8 >> 3;   // elements per stream, 0..16
+  auto pass = [&](bool sq, double mu) -> double {
+    double r[8];
+#pragma unroll 1
+    for (int e0 = 0; e0 < cnt; e0 += 4) {
+      double xv[8][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int uu = e0 + u < cnt ? e0 + u : cnt - 1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j][u] = hv[(8 * uu + j) * 64];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        double acc = e0 > 0 ? r[j] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (e0 + u < cnt) {
+            double x = xv[j][u];
+            if (sq) {
+              x = x - mu;
+              x = x * x;
+            }
+            acc = e0 + u == 0 ? x : acc + x;
+          }
+        }
+        r[j] = acc;
+      }
+    }
+    double res = cnt ? ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7])) : 0.0;
+#pragma unroll 1
+    for (int i = m8; i < G; ++i) {   // the G % 8 tail, in order (G < 8: from 0)
+      double x = hv[i * 64];
+      if (sq) {
+        x = x - mu;
+        x = x * x;
+      }
+      res += x;
+    }
+    return res;
+  };
+  const double tot = pass(false, 0.0);
+  const double mu = tot / G + sdm * hz;                        // mu ~ N(mean(x), sqrt(s2/G))
+  const double ss = pass(true, mu);
+  const double hat = ss / (double)(G - 1);
+  const double scale = d.ha * hat;
+  // scipy invgamma.rvs: (1/gammainccinv(a, U)) * scale + loc; loc when scale == 0
+  const double s2n = scale == 0.0 ? 0.0 : (1.0 / hx) * scale;
+  const double sdn = sqrt(s2n);
+  const double lsd = log(sdn);
+  hy[(NMC_HY_MU * P + p) * 64] = mu;
+  hy[(NMC_HY_SD * P + p) * 64] = sdn;
+  hy[(NMC_HY_LSD * P + p) * 64] = lsd;
+  hy[(NMC_HY_S2 * P + p) * 64] = s2n;
+  hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
+  if (write && c < C) {
+    const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
+    d.mu[ho] = mu;
+    d.s2[ho] = s2n;
+    d.hsd[ho] = sdn;
+    d.hlsd[ho] = lsd;
+    const int row = nmc_record_row(d, t);
+    if (row >= 0) {
+      double* out = d.samples + ((size_t)row * d.cols + (size_t)p * (G + 2)) * C + c;
+      out[0] = mu;
+      out[C] = s2n;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K_run: iterations [i0, i1) for every (chain, group); grid = CB*G workgroups of
-// 64*W threads; dynamic LDS = nmc_lds(...).total columns.
-// Wave roles (W > 1):
+// 64*W threads (W <= 8); dynamic LDS = nmc_lds(...).total columns.
+// Wave roles:
 //   wave 0            control: proposal priors, Metropolis decision, tuning, state,
-//                     sample/trace stores, variate DMA, publishing (no likelihood);
-//   waves 1..NAUX     auxiliary (partial, payload-in-LDS mode): during the step-0
-//                     likelihood they wait for the chain block's values and copy them
-//                     into LDS; on every other step they evaluate likelihood tiles;
-//   remaining waves   likelihood tiles.
-// W == 1: the single wave does everything.
-// Likelihood: each likelihood wave sums a contiguous row range; the control wave adds
-// the partials in a fixed order.  W and the row ranges depend only on (N, P, G), and
-// step 0 of partial pooling always uses the W-1-NAUX non-auxiliary waves, so the
-// sums -- and the chains -- do not depend on the chain-block count, the launch mode
-// or the number of GPUs.
+//                     sample/trace stores, variate DMA, publishing, and (persistent
+//                     payload-in-LDS mode, P >= 2) the Gibbs payload copy;
+//   wave 1 (NAUX = 1) Gibbs update (persistent payload-in-LDS mode): the task the
+//                     control wave copied at the previous step (P == 1: poll, copy
+//                     and update in the same step);
+//   every wave        once its own work is done, takes likelihood row tiles from an
+//                     LDS counter until none is left, so a wave that shares its SIMD
+//                     with a busy control or Gibbs wave simply takes fewer tiles.
+// The control wave adds the 16 tile partials in a fixed order (nmc_tiles): the sums do
+// not depend on which wave took which tile.
 //   flags & NMC_RUN_HYPER_LOAD: the hyper-parameters after iteration i0-1 are in
 //     global memory (chunk start / initial state); otherwise (launch per iteration)
 //     they are recomputed from vb[(i0-1)&1] at step 0 of i0.
@@ -747,9 +792,9 @@ __device__ __forceinline__ void nmc_load_theta(const Dev& d, const double* src, 
 enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
        NMC_MODE_LAUNCH = 1,      // one launch per iteration, plain loads after the boundary
        NMC_MODE_SYNC = 2,        // persistent, sc1 loads after the barrier
-       NMC_MODE_SYNC_LDS = 3 };  // persistent, auxiliary waves copy the payload into LDS
+       NMC_MODE_SYNC_LDS = 3 };  // persistent, the Gibbs wave works on an LDS copy
 template <class Fam, int MODE>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(512)
 nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int flags) {
   constexpr bool PARTIAL = MODE != NMC_MODE_NOPOOL;
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -764,22 +809,25 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const int cc = live ? c : C - 1;
   constexpr bool sync = MODE == NMC_MODE_SYNC || MODE == NMC_MODE_SYNC_LDS;
   constexpr bool hl = MODE == NMC_MODE_SYNC_LDS;  // payload-in-LDS Gibbs update
-  const int naux = d.naux;       // reserved at step 0 of partial pooling in every mode
   const int row_doubles = d.rows_lds ? d.nmax * Fam::NFIELDS : 0;
   const nmc_lds_layout L =
       nmc_lds(Fam::NACC, P, PARTIAL, d.nleaf, d.ntail, W, G, hl ? 1 : 0, row_doubles);
   double* th = lds + L.th * 64 + lane;            // th[p * 64]: this lane's chain, parameter p
   double* st = lds + L.st * 64 + lane;            // st[(k * P + p) * 64]
   double* hy = lds + L.hyp * 64 + lane;           // hy[(k * P + p) * 64]
+  // tile counters, one per step parity (two 32-bit words in the flag column)
+  unsigned* tcnt = (unsigned*)(lds + L.flag * 64 + 4);
   const int64_t r0 = d.off[g];
   const int nrow = (int)(d.off[g + 1] - r0);
+  int nt, tl;
+  nmc_tiles(nrow, d.tile, &nt, &tl);
   const double* grows = obs + r0 * Fam::NFIELDS;
   const size_t PGC = (size_t)P * G * C;
   const size_t gc = (size_t)g * C + cc;
   const bool ctl = w == 0;
-  // latency-bound roles (control, loaders, compute) issue ahead of the likelihood waves
-  // sharing their SIMD, which fill the gaps
-  if (W > 1 && w <= naux && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
+  const bool gw = hl && w == 1;                   // the Gibbs wave
+  // latency-bound roles (control, Gibbs) issue ahead of the waves sharing their SIMD
+  if (W > 1 && (ctl || gw) && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
 
   // ---- prologue: values and state -> LDS (parameter p by wave p % W) ----
   const double* vin = ((i0 - 1) & 1) ? d.vb1 : d.vb0;
@@ -807,7 +855,6 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     }
   }
   const double gcst = fam.gconst((long)nrow);   // per-group constant of finish_fast
-  double LL = d.ll[gc];
   double* lrows = lds + L.rows * 64;
   if (d.rows_lds) {   // this group's rows -> LDS, once for the whole launch
     const int nd = nrow * Fam::NFIELDS;
@@ -816,32 +863,38 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   auto zl_src = [&](int tn, int pn) -> const double* {
     return d.vzl + ((size_t)(tn - d.vbase) * PGC + (size_t)pn * G * C + gc) * 2;
   };
-  const int l0 = W == 1 ? 0 : 1 + naux;   // likelihood waves l0..W-1
-  const int nll = W - l0;
+  double* cwv = lds + L.cw * 64 + lane;    // cwv[k * 64]: control-wave values across barriers
   if (ctl) {     // {z, log u} of the first step -> LDS slot of step i0*P
     nmc_dma16(zl_src(i0, 0), lds + (L.zl + 2 * ((i0 * P) & 1)) * 64);
     for (int j = 0; j < Fam::NACC; ++j)   // x + (-0.0) == x: the fixed 16-slot sum
-      for (int k = nll; k < 16; ++k) lds[(L.part + j * 16 + k) * 64 + lane] = -0.0;
+      for (int k = nt; k < 16; ++k) lds[(L.part + j * 16 + k) * 64 + lane] = -0.0;
     nmc_drain_vm();
-    lds[L.flag * 64 + lane] = 0.0;
+    lds[L.flag * 64 + lane] = 0.0;       // (also zeroes both tile counters)
   }
   __syncthreads();
 
   bool ok = true;
   int pub_p = -1;     // control wave: parameter whose sc1 value store awaits its counter add
   int pend_p = -1, pend_t = 0;   // control wave: decided step whose state update is pending
-  double* cwv = lds + L.cw * 64 + lane;    // cwv[k * 64]
+  // Control-wave values, in registers across the step's barriers (the LDS queue is
+  // saturated by the likelihood tiles while they are produced): the proposal, current
+  // value, log accept uniform and priors of the step, both outcomes of its counters and
+  // scale, the group log-likelihood of the current state, and the decided-but-pending
+  // step's accept flag, log prior and log-likelihood.
+  // (step-local ones are declared inside the step loop, so they are not live across the
+  // Gibbs wave's bursts; the counters' outcomes wait in LDS)
+  double c_LL = ctl ? d.ll[gc] : 0.0;
+  bool q_acc = false;
+  double q_plp = 0, q_pll = 0;
   // the rest of a decided step's state update (:369-383, :608-610): counters, log prior,
   // log-likelihood, sample and trace rows
   auto apply_pending = [&]() {
     const int q = pend_p, tq = pend_t;
-    const bool accept = cwv[NMC_CW_PAC * 64] != 0.0;
-    const double llp = cwv[NMC_CW_PLL * 64];
-    st[(NMC_ST_LP * P + q) * 64] = cwv[NMC_CW_PLP * 64];
-    st[(NMC_ST_NA * P + q) * 64] = cwv[(accept ? NMC_CW_NAA : NMC_CW_NAR) * 64];
-    st[(NMC_ST_NR * P + q) * 64] = cwv[(accept ? NMC_CW_NRA : NMC_CW_NRR) * 64];
-    st[(NMC_ST_TA * P + q) * 64] = cwv[NMC_CW_TA * 64] + (accept ? 1.0 : 0.0);
-    if (accept) LL = llp;
+    st[(NMC_ST_LP * P + q) * 64] = q_plp;
+    st[(NMC_ST_NA * P + q) * 64] = cwv[(q_acc ? NMC_CW_NAA : NMC_CW_NAR) * 64];
+    st[(NMC_ST_NR * P + q) * 64] = cwv[(q_acc ? NMC_CW_NRA : NMC_CW_NRR) * 64];
+    st[(NMC_ST_TA * P + q) * 64] = cwv[NMC_CW_TA * 64] + (q_acc ? 1.0 : 0.0);
+    if (q_acc) c_LL = q_pll;
     if (live) {
       const int row = nmc_record_row(d, tq);
       if (row >= 0) {
@@ -850,8 +903,8 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       }
       if (tq < d.trace_n) {
         const size_t it = (((size_t)tq * P + q) * G + g) * C + c;
-        d.tflag[it] = accept ? 1 : 0;
-        d.tllp[it] = llp;
+        d.tflag[it] = q_acc ? 1 : 0;
+        d.tllp[it] = q_pll;
       }
     }
     pend_p = -1;
@@ -861,44 +914,77 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
     for (int p = 0; p < P; ++p) {
       const int sp = (t * P + p) & 1;
+      double c_prop, c_v, c_lu, c_lpc, c_lpp, c_sA, c_sR;   // control wave, this step
       // Gibbs update of every parameter at step 0 (launch-per-iteration / fallback)
       const bool hyper_now =
           !hl && PARTIAL && p == 0 && t > 0 && !(t == i0 && (flags & NMC_RUN_HYPER_LOAD));
-      // payload-in-LDS: the Gibbs update of parameter q after iteration tq is task
-      // k = tq*P + q; every workgroup publishes it right after its decision at global step
-      // k, so it is counted at the start of step k+1.  P == 1: the auxiliary waves load and
-      // compute task gs-1 at step gs (needed at once).  P >= 2 (two-stage pipeline): the
-      // loader waves copy task gs-1 into LDS buffer (gs-1)&1 at step gs, the compute wave
-      // updates task gs-2 from buffer gs&1 -- needed first at step gs-2+P.
+      // persistent Gibbs wave: the Gibbs update of parameter q after iteration tq is
+      // task k = tq*P + q; every workgroup publishes it right after its decision at
+      // global step k, so it is counted at the start of step k+1.  P == 1: the Gibbs
+      // wave polls, copies and updates task gs-1 at step gs (needed at once).  P >= 2
+      // (two-stage pipeline): the control wave polls task gs-1 at step gs and copies its
+      // payload into LDS buffer (gs-1)&1; the Gibbs wave updates task gs-2 from buffer
+      // gs&1 at step gs, beside the tiles -- needed first at step gs-2+P.
       const int gs = t * P + p, gs0 = i0 * P;
       const bool pipe = hl && P >= 2;
-      const int aq = p > 0 ? p - 1 : P - 1;        // loaders' task: (atq, aq) = gs-1
+      const int aq = p > 0 ? p - 1 : P - 1;        // task gs-1 = (atq, aq)
       const int atq = p > 0 ? t : t - 1;
       const bool aux_now = hl && gs - 1 >= gs0;
-      const bool comp_now = pipe && gs - 2 >= gs0;  // compute wave's task: (ctq, cq) = gs-2
-      const int cq = (p + 2 * P - 2) % (P > 0 ? P : 1);
+      const bool comp_now = pipe && gs - 2 >= gs0;  // Gibbs task gs-2 = (ctq, cq)
+      const int cq = (p + 2 * P - 2) % P;
       const int ctq = p >= 2 ? t : t - 1;
-      // the update of this step's parameter lands during this step (P <= 2): priors
-      // after the barrier
+      // this step's priors come from the Gibbs wave when the update they depend on
+      // lands during this step (P == 1, or P == 2 with the pipeline full)
       const bool post_prior = P == 1 ? aux_now : (P == 2 && comp_now);
-      // proposal (Parameter.propose :304-306): value + (proposalSd=1 * scale) * z
-      const double v = th[p * 64];
-      const double s = st[(NMC_ST_S * P + p) * 64];
-      const double zc = lds[(L.zl + 2 * sp) * 64 + 2 * lane];
-      const double prop = v + (1.0 * s) * zc;
-      // this step's priors (:293-294) from the hyper-parameters in LDS -- by the wave that
-      // has just updated them when that update lands during this step (post_prior)
-      auto step_priors = [&]() {
-        const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
-        const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
-        cwv[NMC_CW_LPC * 64] =
-            t > 0 ? nmc_norm_logpdf_r(v, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
-        cwv[NMC_CW_LPP * 64] = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
-      };
-      // ---- control wave, before the barrier: next variates in flight, priors, and both
-      //      outcomes of the decision -- accept (sA, naA, nrA, ta + 1) / reject (sR,
-      //      naR, nrR, ta), tuned if due -- parked in LDS (no registers live across
-      //      the likelihood region) ----
+      // ---- the Gibbs wave, beside this step's likelihood tiles ----
+      if constexpr (hl) if (gw) {
+        bool upd = false;
+        if (!pipe && aux_now) {   // P == 1: poll task gs-1, copy it, update it
+          const size_t hvi = (((size_t)(atq - d.vbase) * P + aq) * C + cc) * 2;
+          const double hz = d.vh[hvi], hx = d.vh[hvi + 1];
+          const bool r = nmc_poll_published(d, cb, aq, (unsigned)G * (unsigned)(atq - i0 + 1));
+          if (lane == 0)
+            __hip_atomic_store(lds + L.flag * 64 + 1, r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (p == 0) NMC_STAMP_AUX(t, 13);
+          if (r) {
+            // keep the payload loads below the poll (no instruction: wavefront scope)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const double* src = (atq & 1) ? d.vb1 : d.vb0;
+            if ((C & 1) == 0) {
+              nmc_hyper_dma(d, src, aq, cb, 0, G, lds, L, 0);
+              nmc_drain_vm();
+            } else {
+              nmc_hyper_load(d, src, aq, cc, 0, G, lds, L, 0);
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+            nmc_hyper_compute(d, cb, atq, aq, lds, L, g == 0, hz, hx, 0);
+            upd = true;
+          }
+        } else if (comp_now) {   // P >= 2: task gs-2, copied into buffer (gs-2)&1 at step gs-1
+          const size_t hvi = (((size_t)(ctq - d.vbase) * P + cq) * C + cc) * 2;
+          if (p == 0) NMC_STAMP_CMP(t, 13);
+          nmc_hyper_compute(d, cb, ctq, cq, lds, L, g == 0, d.vh[hvi], d.vh[hvi + 1],
+                            (gs & 1) * (G + 1));
+          if (p == 0) NMC_STAMP_CMP(t, 14);
+          upd = post_prior;
+        }
+        if (upd) {   // this step's priors (:293-294) from the update just made
+          const double v = th[p * 64];
+          const double prop = v + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
+                                      lds[(L.zl + 2 * sp) * 64 + 2 * lane];
+          const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
+          const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
+          cwv[NMC_CW_LPC * 64] =
+              t > 0 ? nmc_norm_logpdf_r(v, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
+          cwv[NMC_CW_LPP * 64] = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
+          if (p == 0) NMC_STAMP_CMP(t, 15);
+        }
+      }
+      // ---- control wave: counter add of the last publish, the poll and payload copy of
+      //      task gs-1, the pending state update, both outcomes of the decision --
+      //      accept (sA, naA, nrA, ta + 1) / reject (sR, naR, nrR, ta), tuned if due --,
+      //      the next step's variates in flight, priors ----
       if (ctl) {
         if constexpr (sync) {   // the previous step's value is stored; count it published
           if (pub_p >= 0) {
@@ -909,18 +995,14 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             pub_p = -1;
           }
         }
-        // P >= 2: the control wave is the loader, right after its own publish (the copies
-        // stay in flight under the rest of its pre-barrier work): it waits for the chain
-        // block's counter of task gs-1 (verdict word for the check after barrier A) and
-        // copies the payload into LDS buffer (gs-1)&1 (sc1 LDS-DMA, drained with its other
-        // copies before barrier A)
-        if constexpr (hl) if (pipe && aux_now) {
+        if constexpr (hl) if (pipe && aux_now) {   // verdict word (checked after barrier A), copy
           const bool r = nmc_poll_published(d, cb, aq, (unsigned)G * (unsigned)(atq - i0 + 1));
           if (lane == 0)
             __hip_atomic_store(lds + L.flag * 64 + 1, r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           if (p == 0) NMC_STAMP(t, 8);
           if (r) {
+            // keep the payload loads below the poll (no instruction: wavefront scope)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const double* src = (atq & 1) ? d.vb1 : d.vb0;
             if ((C & 1) == 0)
@@ -930,152 +1012,84 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
           }
         }
         if (pend_p >= 0) apply_pending();
+        c_v = th[p * 64];
+        const double s = st[(NMC_ST_S * P + p) * 64];
+        c_prop = c_v + (1.0 * s) * lds[(L.zl + 2 * sp) * 64 + 2 * lane];   // propose (:304-306)
+        c_lu = lds[(L.zl + 2 * sp) * 64 + 2 * lane + 1];
         {
           const double na = st[(NMC_ST_NA * P + p) * 64], nr = st[(NMC_ST_NR * P + p) * 64];
-          double sA = s, sR = s, naA = na + 1.0, nrA = nr, naR = na, nrR = nr + 1.0;
+          double naA = na + 1.0, nrA = nr, naR = na, nrR = nr + 1.0;
+          c_sA = s;
+          c_sR = s;
           if (tune) {
-            nmc_tune(sA, naA, nrA);
-            nmc_tune(sR, naR, nrR);
+            nmc_tune(c_sA, naA, nrA);
+            nmc_tune(c_sR, naR, nrR);
           }
-          cwv[NMC_CW_SA * 64] = sA;
-          cwv[NMC_CW_SR * 64] = sR;
           cwv[NMC_CW_NAA * 64] = naA;
           cwv[NMC_CW_NRA * 64] = nrA;
           cwv[NMC_CW_NAR * 64] = naR;
           cwv[NMC_CW_NRR * 64] = nrR;
           cwv[NMC_CW_TA * 64] = st[(NMC_ST_TA * P + p) * 64];
         }
-        cwv[NMC_CW_LU * 64] = lds[(L.zl + 2 * sp) * 64 + 2 * lane + 1];
-        cwv[NMC_CW_PROP * 64] = prop;
-        cwv[NMC_CW_V * 64] = v;
         const int tn = p + 1 < P ? t : t + 1;
         const int pn = p + 1 < P ? p + 1 : 0;
         if (tn < i1) nmc_dma16(zl_src(tn, pn), lds + (L.zl + 2 * (sp ^ 1)) * 64);
         if (!hl && hyper_now) nmc_hyper_variates(d, cb, t - 1, lds, L, 0, 1);
         if (PARTIAL && !hl && p == (P > 1 ? 1 : 0)) nmc_hyper_sdm(d, lds, L, lane);
         if (!hyper_now && !(hl && post_prior)) {   // priors (:293-294)
-          double lpc, lpp;
           if (PARTIAL) {
             const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
             const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
-            lpc = t > 0 ? nmc_norm_logpdf_r(v, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
-            lpp = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
+            c_lpc = t > 0 ? nmc_norm_logpdf_r(c_v, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
+            c_lpp = nmc_norm_logpdf_r(c_prop, m, sd, isd, lsd);
           } else {
-            lpc = st[(NMC_ST_LP * P + p) * 64];
-            lpp = nmc_prior_logpdf(d.pfam[p], d.ppar + 8 * p, prop);
+            c_lpc = st[(NMC_ST_LP * P + p) * 64];
+            c_lpp = nmc_prior_logpdf(d.pfam[p], d.ppar + 8 * p, c_prop);
           }
-          cwv[NMC_CW_LPC * 64] = lpc;
-          cwv[NMC_CW_LPP * 64] = lpp;
         }
       }
-      // ---- auxiliary waves, overlapped with this step's likelihood: loader wave 1 waits
-      //      for the chain block's counter of task gs-1, each loader copies its share of
-      //      the groups' values into LDS (one batch of sc1 loads); P == 1: they join
-      //      through LDS epoch words and wave 1 computes; P >= 2: the compute wave (the
-      //      last auxiliary) updates task gs-2 from the buffer the loaders filled at the
-      //      previous step ----
-      const int nload = pipe ? 0 : naux;   // P >= 2: the control wave loads, waves 1-2 compute
-      const bool aux = hl && w >= 1 && w <= naux && (w <= nload ? aux_now : comp_now);
-      if constexpr (hl) if (aux) {
-        const int a = w - 1;
-        if (a < nload) {
-          double hz = 0.0, hx = 0.0;
-          if (!pipe && a == 0) {   // this lane's hyper variates of (atq, aq), issued early
-            const size_t hvi = (((size_t)(atq - d.vbase) * P + aq) * C + cc) * 2;
-            hz = d.vh[hvi];
-            hx = d.vh[hvi + 1];
-          }
-          const double want = 2.0 * ((double)gs + 1);      // this step's epoch
-          double* flagw = lds + L.flag * 64 + 1;
-          if (a == 0) {
-            const bool r = nmc_poll_published(d, cb, aq, (unsigned)G * (unsigned)(atq - i0 + 1));
-            if (lane == 0)
-              __hip_atomic_store(flagw, r ? want : -want, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-          double f;
-          while (true) {
-            f = __hip_atomic_load(flagw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (f == want || f == -want) break;
-            __builtin_amdgcn_s_sleep(1);
-          }
-          // keep the payload loads below the poll (no instruction: wavefront scope)
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          if (p == 0) NMC_STAMP_AUX(t, 13);
-          if (f == want) {
-            const double* src = (atq & 1) ? d.vb1 : d.vb0;
-            if (nload == 1 && (C & 1) == 0) {
-              nmc_hyper_dma(d, src, aq, cb, 0, G, lds, L, ((gs - 1) & 1) * (G + 1));
-              nmc_drain_vm();
-            } else {
-              nmc_hyper_load(d, src, aq, cc, (int)(((int64_t)G * a) / nload),
-                             (int)(((int64_t)G * (a + 1)) / nload), lds, L, ((gs - 1) & 1) * (G + 1));
-            }
-            if (p == 0) NMC_STAMP_AUX(t, 14);
-            if (!pipe) {
-              // join: each loader stamps its LDS word with the epoch once its share has
-              // landed; wave 1 waits for all of them (bounded)
-              double* joinw = lds + L.flag * 64 + 8;
-              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-              if (lane == 0)
-                __hip_atomic_store(joinw + a, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              if (a == 0) {
-                for (int k = 1; k < nload; ++k)
-                  for (unsigned spins = 0;
-                       __hip_atomic_load(joinw + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) !=
-                           want &&
-                       spins < NMC_SPIN_LIMIT;
-                       ++spins)
-                    __builtin_amdgcn_s_sleep(1);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (p == 0) NMC_STAMP_AUX(t, 15);
-                nmc_hyper_compute(d, cb, atq, aq, lds, L, g == 0, hz, hx, ((gs - 1) & 1) * (G + 1));
-                if (post_prior) step_priors();
-                if (p == 0) NMC_STAMP_AUX(t, 12);
-              }
-            }
-          }
-        } else {   // compute waves: task gs-2, loaded into buffer (gs-2)&1 at step gs-1
-          const int half = w - nload - 1;
-          const size_t hvi = (((size_t)(ctq - d.vbase) * P + cq) * C + cc) * 2;
-          if (p == 0) NMC_STAMP_CMP(t, 13);
-          if (G >= 8)
-            nmc_hyper_compute2(d, cb, ctq, cq, lds, L, g == 0, d.vh[hvi], d.vh[hvi + 1],
-                               (gs & 1) * (G + 1), half, (double)(gs + 1));
-          else if (half == 0)
-            nmc_hyper_compute(d, cb, ctq, cq, lds, L, g == 0, d.vh[hvi], d.vh[hvi + 1],
-                              (gs & 1) * (G + 1));
-          if (p == 0) NMC_STAMP_CMP(t, 14);
-          if (post_prior && half == 0) step_priors();
-          if (p == 0) NMC_STAMP_CMP(t, 15);
-        }
-      }
-      // ---- likelihood of the proposal over this wave's rows (:615-635) ----
-      if (w >= l0 && !aux) {
-        const int k = w - l0;
-        int64_t ra;
-        int rn;
-        nmc_chunk(0, nrow, k, nll, &ra, &rn);
+      // ---- likelihood of the proposal (:615-635), tile by tile, every wave ----
+      {
         double thp[Fam::MAXP];
 #pragma unroll
-        for (int q = 0; q < Fam::MAXP; ++q) thp[q] = q < P ? (q == p ? prop : th[q * 64]) : 0.0;
-        const typename Fam::Reg reg = fam.prepare(thp);
-        double acc[Fam::NACC];
-        if (d.rows_lds)   // wave-uniform LDS address: broadcast ds_reads, software-pipelined
-          nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
-        else              // wave-uniform global address: scalar loads
-          nmc_ll_rows(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, acc);
+        for (int q = 0; q < Fam::MAXP; ++q) thp[q] = q < P ? th[q * 64] : 0.0;
+        const double prop = thp[p] + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
+                                         lds[(L.zl + 2 * sp) * 64 + 2 * lane];
 #pragma unroll
-        for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * 16 + k) * 64 + lane] = acc[j];
+        for (int q = 0; q < Fam::MAXP; ++q)
+          if (q == p) thp[q] = prop;
+        const typename Fam::Reg reg = fam.prepare(thp);
+        // the next tile is requested before the current one is computed: the atomic's
+        // return rides under the tile's own row reads
+        auto grab = [&]() -> unsigned {
+          unsigned k = 0;
+          if (lane == 0)
+            k = __hip_atomic_fetch_add(tcnt + sp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          return k;
+        };
+        int k = (int)__builtin_amdgcn_readlane(grab(), 0);
+        while (k < nt) {
+          const unsigned kn = grab();
+          const int ra = k * tl;
+          const int rn = (k + 1 == nt ? nrow : ra + tl) - ra;
+          double acc[Fam::NACC];
+          if (d.rows_lds)   // wave-uniform LDS address: broadcast ds_reads, software-pipelined
+            nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
+          else              // wave-uniform global address: scalar loads
+            nmc_ll_rows(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, acc);
+#pragma unroll
+          for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * 16 + k) * 64 + lane] = acc[j];
+          k = (int)__builtin_amdgcn_readlane(kn, 0);
+        }
       }
       NMC_STAMP(t, 1 + 3 * (p & 1));
-      if (ctl) nmc_drain_vm();   // this wave's LDS-DMA has landed
+      if (ctl || (hl && !pipe && gw)) nmc_drain_vm();   // this wave's LDS-DMA has landed
       __syncthreads();
       NMC_STAMP(t, 2 + 3 * (p & 1));
 
       // ---- Gibbs update after iteration t-1 (needed by this iteration's priors) ----
       if constexpr (hl) {
-        if (aux_now) {   // the loaders' verdict
+        if (aux_now) {   // the poller's verdict
           ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
           if (!ok) break;
         }
@@ -1091,9 +1105,8 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         if (ctl) {
           const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
           const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
-          const double vv = cwv[NMC_CW_V * 64], pp = cwv[NMC_CW_PROP * 64];
-          cwv[NMC_CW_LPC * 64] = nmc_norm_logpdf_r(vv, m, sd, isd, lsd);   // t > 0 (setPrior :281)
-          cwv[NMC_CW_LPP * 64] = nmc_norm_logpdf_r(pp, m, sd, isd, lsd);
+          c_lpc = nmc_norm_logpdf_r(c_v, m, sd, isd, lsd);   // t > 0 (setPrior :281)
+          c_lpp = nmc_norm_logpdf_r(c_prop, m, sd, isd, lsd);
         }
         NMC_STAMP(t, 9);
       }
@@ -1101,12 +1114,13 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       // ---- control wave: group log-likelihood of the proposal (tiles in order) and
       //      the Metropolis decision, one chain per lane (:334-383) ----
       if (ctl) {
+        if (lane == 0) tcnt[sp] = 0u;   // this step's tiles are all taken; reused at step +2
         double acc[Fam::NACC];
 #pragma unroll
         for (int j = 0; j < Fam::NACC; ++j) {
-          // the likelihood waves' partials in a fixed order: wave k into accumulator
-          // k % 4, combined (a0+a1)+(a2+a3); every LDS read in flight at once (slots
-          // past the last likelihood wave hold -0.0)
+          // the tile partials in a fixed order: tile k into accumulator k % 4, combined
+          // (a0+a1)+(a2+a3); every LDS read in flight at once (slots past the last tile
+          // hold -0.0)
           const double* pt = lds + (L.part + j * 16) * 64 + lane;
           double a4[4] = {0.0, 0.0, 0.0, 0.0};
           double v16[16];
@@ -1118,25 +1132,26 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
           acc[j] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
         }
         if (p == 0) NMC_STAMP(t, 10);
-        const double prop = cwv[NMC_CW_PROP * 64], v = cwv[NMC_CW_V * 64];
-        const double lpc = cwv[NMC_CW_LPC * 64], lpp = cwv[NMC_CW_LPP * 64];
-        const double lu = cwv[NMC_CW_LU * 64];
         double thp[Fam::MAXP];
 #pragma unroll
-        for (int q = 0; q < Fam::MAXP; ++q) thp[q] = q < P ? (q == p ? prop : th[q * 64]) : 0.0;
+        for (int q = 0; q < Fam::MAXP; ++q) thp[q] = q < P ? (q == p ? c_prop : th[q * 64]) : 0.0;
         const typename Fam::Reg reg = fam.prepare(thp);
         const double llp = fam.finish_fast(reg, acc, (long)nrow, gcst);
         if (p == 0) NMC_STAMP(t, 11);
-        const double postp = lpp + llp;
-        const double post = lpc + LL;
+        if (hl && post_prior) {   // the Gibbs wave evaluated this step's priors
+          c_lpc = cwv[NMC_CW_LPC * 64];
+          c_lpp = cwv[NMC_CW_LPP * 64];
+        }
+        const double postp = c_lpp + llp;
+        const double post = c_lpc + c_LL;
         const double diff = postp - post;
         bool accept;
         if (!isfinite(post) && isfinite(postp)) accept = true;        // :347-352
         else if (!isfinite(llp)) accept = false;                      // :354-356
         else if (!isfinite(diff)) accept = false;                     // :358-360
-        else accept = lu < diff;                                      // :362-364
+        else accept = c_lu < diff;                                    // :362-364
         // :369-383, :608-610 (+ tune :385-437, prepared above)
-        const double vn = accept ? prop : v;
+        const double vn = accept ? c_prop : c_v;
         th[p * 64] = vn;
         if constexpr (sync) {   // publish write-through; counted at the next step's start
           if (live)
@@ -1144,10 +1159,10 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           pub_p = p;
         }
-        st[(NMC_ST_S * P + p) * 64] = cwv[(accept ? NMC_CW_SA : NMC_CW_SR) * 64];
-        cwv[NMC_CW_PAC * 64] = accept ? 1.0 : 0.0;
-        cwv[NMC_CW_PLP * 64] = accept ? lpp : lpc;
-        cwv[NMC_CW_PLL * 64] = llp;
+        st[(NMC_ST_S * P + p) * 64] = accept ? c_sA : c_sR;
+        q_acc = accept;
+        q_plp = accept ? c_lpp : c_lpc;
+        q_pll = llp;
         pend_p = p;
         pend_t = t;
         // the rest of the update waits for the next step's pre-barrier slack
@@ -1181,35 +1196,28 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       d.nrej[ip] = (int)st[(NMC_ST_NR * P + p) * 64];
       d.tacc[ip] = (long long)st[(NMC_ST_TA * P + p) * 64];
     }
-    d.ll[gc] = LL;
+    d.ll[gc] = c_LL;
   }
-  // ---- closing Gibbs update after i1-1 (group-0 workgroups write and record it) ----
+  // ---- closing Gibbs updates after i1-1 (group-0 workgroups write and record them) ----
   if constexpr (hl) if (ok && g == 0) {
-    const int ge = i1 * P;   // tasks ge-2 (loaded at the last step; P >= 2) and ge-1 are left
-    const bool pipe = P >= 2;
-    const int nload = 1;   // closing: wave 1 loads
-    if (pipe && w == naux) {
+    const int ge = i1 * P;   // tasks ge-2 (copied at the last step; P >= 2) and ge-1 are left
+    if (P >= 2 && gw) {
       const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 2)) * C + cc) * 2;
       nmc_hyper_compute(d, cb, i1 - 1, P - 2, lds, L, true, d.vh[hvi], d.vh[hvi + 1],
                         ((ge - 2) & 1) * (G + 1));
     }
-    if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L)) {
-      if (w >= 1 && w <= nload) {
-        const double* src = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
-        if (nload == 1 && (C & 1) == 0) {
-          nmc_hyper_dma(d, src, P - 1, cb, 0, G, lds, L, ((ge - 1) & 1) * (G + 1));
-          nmc_drain_vm();
-        } else {
-          nmc_hyper_load(d, src, P - 1, cc, (int)(((int64_t)G * (w - 1)) / nload),
-                         (int)(((int64_t)G * w) / nload), lds, L, ((ge - 1) & 1) * (G + 1));
-        }
+    if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L) && gw) {
+      const double* src = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
+      const int ho = ((ge - 1) & 1) * (G + 1);
+      if ((C & 1) == 0) {
+        nmc_hyper_dma(d, src, P - 1, cb, 0, G, lds, L, ho);
+        nmc_drain_vm();
+      } else {
+        nmc_hyper_load(d, src, P - 1, cc, 0, G, lds, L, ho);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
-      __syncthreads();
-      if (w == 1) {
-        const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 1)) * C + cc) * 2;
-        nmc_hyper_compute(d, cb, i1 - 1, P - 1, lds, L, true, d.vh[hvi], d.vh[hvi + 1],
-                          ((ge - 1) & 1) * (G + 1));
-      }
+      const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 1)) * C + cc) * 2;
+      nmc_hyper_compute(d, cb, i1 - 1, P - 1, lds, L, true, d.vh[hvi], d.vh[hvi + 1], ho);
     }
   }
   if constexpr (sync && !hl) if (ok && g == 0) {

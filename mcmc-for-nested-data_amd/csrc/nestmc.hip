@@ -46,31 +46,31 @@ static void dfree(nmc_ctx* x, void* p) {
     if (q == p) { hipFree(q); q = nullptr; }
 }
 
-// Waves per workgroup from the rows per group only (>= 64 rows per likelihood wave,
-// at most 16): the likelihood partition -- and so every sum -- is then the same for
-// any chain count, launch mode or GPU count.  Partial pooling reserves NAUX waves at
-// step 0 for the Gibbs update (they compute it in persistent payload-in-LDS mode).
+// Waves per workgroup: one per 64 rows of the largest group plus the control wave
+// (and the Gibbs wave under partial pooling), at most 8 (one 512-thread workgroup per
+// CU, 256 VGPRs per lane): the row loop is LDS-broadcast bound at ~5 cycles per row
+// from 5 waves on (tools/llbench4.hip, profiles/llbench4_r02.json), so more waves only
+// cost registers.  Every wave takes likelihood tiles once its own role is done; the
+// tile partition depends on the group's rows alone (nmc_tiles), so W, NAUX and the
+// launch mode never change a sum.
 static void choose_geometry(nmc_ctx* x) {
   Dev& d = x->d;
   int64_t w = 1 + (d.nmax + 63) / 64;
-  if (w > 16) w = 16;
+  if (x->pooling == NMC_POOL_PARTIAL && w >= 2) w += 1;
+  if (w > 8) w = 8;
   if (w < 1) w = 1;
   if (const char* e = getenv("NMC_WAVES")) {
     const int v = atoi(e);
-    if (v >= 1 && v <= 16) w = v;
+    if (v >= 1 && v <= 8) w = v;
   }
   d.W = (int)w;
-  // partial pooling: P >= 2: two compute waves (the control wave loads the payload
-  // by LDS-DMA); P == 1: one wave loads and computes; reserved in every partial mode so the likelihood
-  // partition (W - 1 - NAUX waves) is the same whatever the launch mode
-  d.naux = 0;
-  if (x->pooling == NMC_POOL_PARTIAL) {
-    // (+2 compute waves when P >= 2: the update is pipelined over two steps and split
-    // over two waves); NAUX does
-    // not depend on C, so neither does the likelihood partition
-    const int na = d.P >= 2 ? 2 : 1;
-    if (d.W >= na + 2 && d.G <= 128) d.naux = na;
+  d.tile = 64;   // rows per likelihood tile (a multiple of 16); diagnostics override below
+  if (const char* e = getenv("NMC_TILE_ROWS")) {
+    const int v = atoi(e);
+    if (v >= 16 && v % 16 == 0) d.tile = v;
   }
+  // partial pooling, persistent payload-in-LDS mode: wave 1 is the Gibbs wave
+  d.naux = x->pooling == NMC_POOL_PARTIAL && d.W >= 3 && d.G <= 128 ? 1 : 0;
   // rows in LDS when they fit beside the rest of the carve (64 KiB for the rows)
   d.rows_lds = (size_t)d.nmax * x->nf * 8 <= (size_t)64 * 1024 &&
                lds_bytes_for(x, 0, 1) <= (size_t)96 * 1024 &&
@@ -190,9 +190,10 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   rc |= dalloc(x, &dobs, (size_t)n_obs * n_fields);
   rc |= dalloc(x, &pf, n_params);
   rc |= dalloc(x, &pp, (size_t)8 * n_params);
-  // (+128 slack: the Gibbs payload DMA reads whole 64-chain rows of the last group)
-  rc |= dalloc(x, &d.vb0, PGC + 128);
-  rc |= dalloc(x, &d.vb1, PGC + 128);
+  // (+72 C + 128 slack: the Gibbs wave reads 72 groups' values unconditionally, and the
+  // payload copies read whole 64-chain rows of the last group)
+  rc |= dalloc(x, &d.vb0, PGC + (size_t)72 * n_chains + 128);
+  rc |= dalloc(x, &d.vb1, PGC + (size_t)72 * n_chains + 128);
   rc |= dalloc(x, &d.lp, PGC);
   rc |= dalloc(x, &d.ll, GC);
   rc |= dalloc(x, &d.scale, PGC);
