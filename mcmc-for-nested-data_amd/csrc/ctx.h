@@ -57,8 +57,9 @@ static inline double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->
 
 static inline size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
   const Dev& d = x->d;
+  // (register hand-off: no LDS payload buffers)
   return (size_t)nmc_lds(x->nacc, d.P, x->pooling == NMC_POOL_PARTIAL, d.nleaf, d.ntail, d.W,
-                         d.G, hlds, rows_lds ? d.nmax * x->nf : 0)
+                         d.G, hlds && !d.hreg, rows_lds ? d.nmax * x->nf : 0)
              .total * 512;
 }
 static inline size_t run_lds_bytes(const nmc_ctx* x) {
@@ -68,7 +69,8 @@ static inline size_t run_lds_bytes(const nmc_ctx* x) {
 static inline int run_mode(const nmc_ctx* x) {
   if (x->pooling != NMC_POOL_PARTIAL) return NMC_MODE_NOPOOL;
   if (!x->persistent) return NMC_MODE_LAUNCH;
-  return x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
+  if (!x->d.hlds) return NMC_MODE_SYNC;
+  return x->d.hreg ? NMC_MODE_SYNC_REG : NMC_MODE_SYNC_LDS;
 }
 
 static inline int pop_event_pair(nmc_ctx* x, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v,

@@ -70,6 +70,7 @@ struct Dev {
   int nleaf, nmerge, ntail;
   int nmax;              // rows of the largest group
   int hlds, naux;        // persistent partial: Gibbs payload via LDS, auxiliary waves
+  int hreg;              // persistent partial, G <= 64: Gibbs payload in registers (SYNC_REG)
   int noprio;            // diagnostics: no issue priority for the latency-bound waves
   int rows_lds;          // 1: each workgroup stages its group's rows in LDS once per launch
   int tile;              // target rows per likelihood tile (nmc_tiles)
@@ -766,6 +767,111 @@ __device__ __forceinline__ void nmc_hyper_compute(const Dev& d, int cb, int t, i
   }
 }
 
+// numpy's pairwise sum (the order of nmc_hyper_compute's pass) over x[0..G) held in
+// registers, G <= 64: every index is a compile-time constant, the G-dependent parts
+// are wave-uniform branches (cnt blocks of 8, the G % 8 tail picked by m8).
+__device__ __forceinline__ double nmc_pairwise_reg(const double (&x)[64], int G, bool sq,
+                                                   double mu) {
+  const int m8 = G >= 8 ? G - G % 8 : 0;
+  const int cnt = m8 >> 3;   // 0..8 blocks of 8
+  auto tr = [&](double v) {
+    if (sq) {
+      v = v - mu;
+      v = v * v;
+    }
+    return v;
+  };
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = tr(x[j]);
+  if (G == 64) {   // eight full blocks, no tail: no selects (the general path below is
+                   // if-converted into a v_cndmask per element and block)
+#pragma unroll
+    for (int u = 1; u < 8; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = r[j] + tr(x[8 * u + j]);
+    return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  }
+#pragma unroll
+  for (int u = 1; u < 8; ++u)
+    if (u < cnt) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = r[j] + tr(x[8 * u + j]);
+    }
+  double res = cnt ? ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7])) : 0.0;
+  double tv[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) tv[k] = 0.0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (8 * u == m8) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) tv[k] = x[8 * u + k < 64 ? 8 * u + k : 63];
+    }
+  const int nt = G - m8;   // the G % 8 tail, in order (G < 8: the whole sum from 0)
+#pragma unroll
+  for (int k = 0; k < 7; ++k)
+    if (k < nt) res += tr(tv[k]);
+  return res;
+}
+
+// The Gibbs update of parameter p after iteration t for this wave's 64 chains from the
+// chain block's values x[0..G) of p in registers (G <= 64); otherwise identical to
+// nmc_hyper_compute (same sums in the same order, same draws, same outputs).
+__device__ __forceinline__ void nmc_hyper_compute_reg(const Dev& d, int cb, int t, int p,
+                                                      double* lds, const nmc_lds_layout& L,
+                                                      bool write, double hz, double hx,
+                                                      const double (&x)[64]) {
+  const int lane = threadIdx.x & 63;
+  const int P = d.P, G = d.G, C = d.C;
+  const int c = cb * 64 + lane;
+  double* hy = lds + L.hyp * 64 + lane;
+  const double sdm = sqrt(hy[(NMC_HY_S2 * P + p) * 64] / G);
+  const double tot = nmc_pairwise_reg(x, G, false, 0.0);
+  const double mu = tot / G + sdm * hz;                        // mu ~ N(mean(x), sqrt(s2/G))
+  const double ss = nmc_pairwise_reg(x, G, true, mu);
+  const double hat = ss / (double)(G - 1);
+  const double scale = d.ha * hat;
+  // scipy invgamma.rvs: (1/gammainccinv(a, U)) * scale + loc; loc when scale == 0
+  const double s2n = scale == 0.0 ? 0.0 : (1.0 / hx) * scale;
+  const double sdn = sqrt(s2n);
+  const double lsd = log(sdn);
+  hy[(NMC_HY_MU * P + p) * 64] = mu;
+  hy[(NMC_HY_SD * P + p) * 64] = sdn;
+  hy[(NMC_HY_LSD * P + p) * 64] = lsd;
+  hy[(NMC_HY_S2 * P + p) * 64] = s2n;
+  hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
+  if (write && c < C) {
+    const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
+    d.mu[ho] = mu;
+    d.s2[ho] = s2n;
+    d.hsd[ho] = sdn;
+    d.hlsd[ho] = lsd;
+    const int row = nmc_record_row(d, t);
+    if (row >= 0) {
+      double* out = d.samples + ((size_t)row * d.cols + (size_t)p * (G + 2)) * C + c;
+      out[0] = mu;
+      out[C] = s2n;
+    }
+  }
+}
+
+// Poll-free half of the register Gibbs hand-off: the chain block's published values of
+// parameter q after iteration tq -> x[0..64) (sc1 loads, all in flight at once: one
+// global round trip, no LDS traffic beside the likelihood waves' broadcasts; x[G..64)
+// read the buffers' 72-group slack or the next parameter and are never summed), and
+// the update's variates {hyper z, gamma}.
+__device__ __forceinline__ void nmc_hyper_fetch_reg(const Dev& d, int tq, int q, int cc,
+                                                    double (&x)[64], double& hz, double& hx) {
+  const int G = d.G, C = d.C;
+  const double* src = ((tq & 1) ? d.vb1 : d.vb0) + (size_t)q * G * C + cc;
+#pragma unroll
+  for (int k = 0; k < 64; ++k) x[k] = nmc_ldv<NMC_SRC_SC1>(src + (size_t)k * C);
+  const size_t hvi = (((size_t)(tq - d.vbase) * d.P + q) * C + cc) * 2;
+  hz = d.vh[hvi];
+  hx = d.vh[hvi + 1];
+}
+
 // ---------------------------------------------------------------------------
 // K_run: iterations [i0, i1) for every (chain, group); grid = CB*G workgroups of
 // 64*W threads (W <= 8); dynamic LDS = nmc_lds(...).total columns.
@@ -792,7 +898,9 @@ __device__ __forceinline__ void nmc_hyper_compute(const Dev& d, int cb, int t, i
 enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
        NMC_MODE_LAUNCH = 1,      // one launch per iteration, plain loads after the boundary
        NMC_MODE_SYNC = 2,        // persistent, sc1 loads after the barrier
-       NMC_MODE_SYNC_LDS = 3 };  // persistent, the Gibbs wave works on an LDS copy
+       NMC_MODE_SYNC_LDS = 3,    // persistent, the Gibbs wave works on an LDS copy
+       NMC_MODE_SYNC_REG = 4 };  // persistent, G <= 64: the Gibbs wave fetches the task's
+                                 // values straight into registers and updates in one step
 template <class Fam, int MODE>
 __global__ void __launch_bounds__(512)
 nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int flags) {
@@ -807,11 +915,19 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const int c = cb * 64 + lane;
   const bool live = c < C;
   const int cc = live ? c : C - 1;
-  constexpr bool sync = MODE == NMC_MODE_SYNC || MODE == NMC_MODE_SYNC_LDS;
-  constexpr bool hl = MODE == NMC_MODE_SYNC_LDS;  // payload-in-LDS Gibbs update
+  constexpr bool sync =
+      MODE == NMC_MODE_SYNC || MODE == NMC_MODE_SYNC_LDS || MODE == NMC_MODE_SYNC_REG;
+  // Gibbs-wave modes: payload in LDS (two-stage pipeline) or in registers (one stage)
+  constexpr bool hr = MODE == NMC_MODE_SYNC_REG;
+  constexpr bool hl = MODE == NMC_MODE_SYNC_LDS || hr;
+  // the Gibbs wave's task at global step gs is gs - lag; the register mode updates a
+  // task two steps after its publication (P >= 2: the hand-off latency -- store drain,
+  // counter add, poll -- is behind a whole step) and the priors that need it come from
+  // the Gibbs wave when it lands in the step that uses it (P <= 2)
+  const int lag = hr && P >= 2 ? 2 : 1;
   const int row_doubles = d.rows_lds ? d.nmax * Fam::NFIELDS : 0;
   const nmc_lds_layout L =
-      nmc_lds(Fam::NACC, P, PARTIAL, d.nleaf, d.ntail, W, G, hl ? 1 : 0, row_doubles);
+      nmc_lds(Fam::NACC, P, PARTIAL, d.nleaf, d.ntail, W, G, hl && !hr ? 1 : 0, row_doubles);
   double* th = lds + L.th * 64 + lane;            // th[p * 64]: this lane's chain, parameter p
   double* st = lds + L.st * 64 + lane;            // st[(k * P + p) * 64]
   double* hy = lds + L.hyp * 64 + lane;           // hy[(k * P + p) * 64]
@@ -909,6 +1025,70 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     }
     pend_p = -1;
   };
+  // ---- register mode: the Gibbs wave runs its own loop (no likelihood tiles), so its
+  //      64-value payload never shares registers with the control and tile code; it
+  //      meets the other waves at the same two barriers per step ----
+  if constexpr (hr) if (gw) {
+    const int gs0 = i0 * P;
+    for (int t = i0; t < i1 && ok; ++t) {
+      for (int p = 0; p < P; ++p) {
+        const int gs = t * P + p;
+        const bool due = gs - lag >= gs0;
+        if (due) {   // task k = gs - lag = (kt, kq): poll, fetch, update
+          const int k = gs - lag, kq = k % P, kt = k / P;
+          const bool r = nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1));
+          if (lane == 0)
+            __hip_atomic_store(lds + L.flag * 64 + 1, r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (p == 0) NMC_STAMP_AUX(t, 13);
+          if (r) {
+            // keep the payload loads below the poll (no instruction: wavefront scope)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double xv[64], fz, fx;
+            nmc_hyper_fetch_reg(d, kt, kq, cc, xv, fz, fx);
+#ifdef NMC_STAMPS
+            nmc_drain_vm();
+            if (p == 0) NMC_STAMP_AUX(t, 14);
+#endif
+            nmc_hyper_compute_reg(d, cb, kt, kq, lds, L, g == 0, fz, fx, xv);
+            if (p == 0) NMC_STAMP_AUX(t, 15);
+            if (P <= 2) {   // the update lands in the step that needs it: this step's priors
+              const int sp = gs & 1;
+              const double v = th[p * 64];
+              const double prop = v + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
+                                          lds[(L.zl + 2 * sp) * 64 + 2 * lane];
+              const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
+              const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
+              cwv[NMC_CW_LPC * 64] =
+                  t > 0 ? nmc_norm_logpdf_r(v, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
+              cwv[NMC_CW_LPP * 64] = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
+            }
+          }
+        }
+        __syncthreads();   // A
+        if (due) {
+          ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
+          if (!ok) break;
+        }
+        __syncthreads();   // B
+      }
+    }
+    // closing: tasks ge-lag .. ge-1 (group-0 workgroups write and record them); the same
+    // barrier as the other waves' nmc_wait_published
+    if (ok && g == 0) {
+      const int ge = i1 * P;
+      if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L)) {
+        for (int k = ge - lag > gs0 ? ge - lag : gs0; k < ge; ++k) {
+          double xv[64], fz, fx;
+          nmc_hyper_fetch_reg(d, k / P, k % P, cc, xv, fz, fx);
+          nmc_hyper_compute_reg(d, cb, k / P, k % P, lds, L, true, fz, fx, xv);
+        }
+      }
+    }
+    nmc_drain_vm();
+    return;
+  }
+
   for (int t = i0; t < i1 && ok; ++t) {
     NMC_STAMP(t, 0);
     const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
@@ -926,18 +1106,19 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       // payload into LDS buffer (gs-1)&1; the Gibbs wave updates task gs-2 from buffer
       // gs&1 at step gs, beside the tiles -- needed first at step gs-2+P.
       const int gs = t * P + p, gs0 = i0 * P;
-      const bool pipe = hl && P >= 2;
+      const bool pipe = hl && !hr && P >= 2;   // two-stage (payload-in-LDS) hand-off
       const int aq = p > 0 ? p - 1 : P - 1;        // task gs-1 = (atq, aq)
       const int atq = p > 0 ? t : t - 1;
-      const bool aux_now = hl && gs - 1 >= gs0;
+      const bool aux_now = hl && gs - lag >= gs0;   // the Gibbs wave's task this step
       const bool comp_now = pipe && gs - 2 >= gs0;  // Gibbs task gs-2 = (ctq, cq)
       const int cq = (p + 2 * P - 2) % P;
       const int ctq = p >= 2 ? t : t - 1;
       // this step's priors come from the Gibbs wave when the update they depend on
       // lands during this step (P == 1, or P == 2 with the pipeline full)
-      const bool post_prior = P == 1 ? aux_now : (P == 2 && comp_now);
-      // ---- the Gibbs wave, beside this step's likelihood tiles ----
-      if constexpr (hl) if (gw) {
+      const bool post_prior =
+          hr ? P <= 2 && aux_now : (P == 1 ? aux_now : (P == 2 && comp_now));
+      // ---- the Gibbs wave, beside this step's likelihood tiles (LDS payload modes) ----
+      if constexpr (hl && !hr) if (gw) {
         bool upd = false;
         if (!pipe && aux_now) {   // P == 1: poll task gs-1, copy it, update it
           const size_t hvi = (((size_t)(atq - d.vbase) * P + aq) * C + cc) * 2;
@@ -1201,12 +1382,14 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   // ---- closing Gibbs updates after i1-1 (group-0 workgroups write and record them) ----
   if constexpr (hl) if (ok && g == 0) {
     const int ge = i1 * P;   // tasks ge-2 (copied at the last step; P >= 2) and ge-1 are left
-    if (P >= 2 && gw) {
+    if (!hr && P >= 2 && gw) {
       const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 2)) * C + cc) * 2;
       nmc_hyper_compute(d, cb, i1 - 1, P - 2, lds, L, true, d.vh[hvi], d.vh[hvi + 1],
                         ((ge - 2) & 1) * (G + 1));
     }
-    if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L) && gw) {
+    // (register mode: the Gibbs wave closes in its own loop; this is the matching barrier)
+    const bool pub = nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L);
+    if (!hr && pub && gw) {
       const double* src = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
       const int ho = ((ge - 1) & 1) * (G + 1);
       if ((C & 1) == 0) {

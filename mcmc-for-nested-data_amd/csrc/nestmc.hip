@@ -80,6 +80,9 @@ static void choose_geometry(nmc_ctx* x) {
   d.noprio = getenv("NMC_NOPRIO") ? atoi(getenv("NMC_NOPRIO")) : 0;   // diagnostics bits
   d.hlds = d.naux > 0 && d.G <= 128 && lds_bytes_for(x, 1, d.rows_lds) <= (size_t)160 * 1024 &&
            !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
+  // G <= 64: the Gibbs wave fetches a task's values into registers (one sc1 round trip)
+  // and updates in the step after publication (no LDS payload, no two-stage pipeline)
+  d.hreg = d.hlds && d.G <= 64 && !(getenv("NMC_NO_HREG") && atoi(getenv("NMC_NO_HREG")));
 }
 
 // numpy's pairwise-sum recursion over G groups (numpy/_core/src/umath/loops_utils.h):
