@@ -14,6 +14,7 @@
 
 #include "../../include/nestmc.h"
 #include "kernels.h"
+#include "pair.h"
 
 // error message of the calling thread (nestmc.hip); returns code
 int nmc_fail(int code, const std::string& msg);
@@ -62,15 +63,21 @@ static inline size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
                          d.G, hlds && !d.hreg, rows_lds ? d.nmax * x->nf : 0)
              .total * 512;
 }
-static inline size_t run_lds_bytes(const nmc_ctx* x) {
-  return lds_bytes_for(x, x->persistent && x->d.hlds ? 1 : 0, x->d.rows_lds);
+static inline size_t pair_lds_bytes(const nmc_ctx* x) {
+  return (size_t)nmc_pair_lds(x->nacc, x->d.nmax * x->nf).total * 512;
 }
 
 static inline int run_mode(const nmc_ctx* x) {
   if (x->pooling != NMC_POOL_PARTIAL) return NMC_MODE_NOPOOL;
   if (!x->persistent) return NMC_MODE_LAUNCH;
+  if (x->d.pair) return NMC_MODE_PAIR;
   if (!x->d.hlds) return NMC_MODE_SYNC;
   return x->d.hreg ? NMC_MODE_SYNC_REG : NMC_MODE_SYNC_LDS;
+}
+
+static inline size_t run_lds_bytes(const nmc_ctx* x) {
+  if (run_mode(x) == NMC_MODE_PAIR) return pair_lds_bytes(x);
+  return lds_bytes_for(x, x->persistent && x->d.hlds ? 1 : 0, x->d.rows_lds);
 }
 
 static inline int pop_event_pair(nmc_ctx* x, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v,

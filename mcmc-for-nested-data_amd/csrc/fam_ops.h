@@ -29,6 +29,10 @@ static int nmc_launch_run(nmc_ctx* x, const Fam& fam, int i0, int i1, int flags)
       hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC>), grid, block, lds, x->stream, d, fam,
                          d.obs, i0, i1, flags);
       break;
+    case NMC_MODE_PAIR:
+      hipLaunchKernelGGL((nmc_k_pair<Fam>), grid, block, lds, x->stream, d, fam, d.obs, i0, i1,
+                         flags);
+      break;
     case NMC_MODE_SYNC_REG:
       hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC_REG>), grid, block, lds, x->stream, d, fam,
                          d.obs, i0, i1, flags);
@@ -49,11 +53,12 @@ template <class Fam>
 static bool nmc_can_persist(nmc_ctx* x) {
   if (const char* e = getenv("NMC_PERSIST")) return atoi(e) != 0;
   int nb = 0;
-  const void* k = !x->d.hlds  ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC>
-                  : x->d.hreg ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_REG>
-                              : (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_LDS>;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W,
-                                                   lds_bytes_for(x, x->d.hlds, x->d.rows_lds)) !=
+  const void* k = x->d.pair   ? (const void*)nmc_k_pair<Fam>
+                  : !x->d.hlds ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC>
+                  : x->d.hreg  ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_REG>
+                               : (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_LDS>;
+  const size_t lds = x->d.pair ? pair_lds_bytes(x) : lds_bytes_for(x, x->d.hlds, x->d.rows_lds);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W, lds) !=
       hipSuccess)
     return false;
   const int safe = nb > 1 ? nb - 1 : nb;

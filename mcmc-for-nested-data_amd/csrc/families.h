@@ -50,29 +50,28 @@ struct FamLinreg {
     r.sig = sigma_known > 0.0 ? sigma_known : (intercept ? th[K + 1] : th[K]);
     return r;
   }
+  // residual e = (b0 - y) + sum_j x_j b_j, accumulated with fmas from the intercept side
+  // (every likelihood path -- LDS asm loop, pair loop, scalar loop -- forms the same e)
   __device__ __forceinline__ void accum(const Reg& r, const double* __restrict__ row,
                                         double* acc) const {
-    double yh = r.b0;
+    double e = r.b0 - row[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) yh = fma(row[j], r.b[j], yh);
-    const double e = yh - row[K];
+    for (int j = 0; j < K; ++j) e = fma(row[j], r.b[j], e);
     acc[0] = fma(e, e, acc[0]);
   }
   // N rows, written stage by stage so the N dependence chains interleave
   template <int N>
   __device__ __forceinline__ void accumN(const Reg& r, const double* __restrict__ rows,
                                          double (&a)[4][NACC]) const {
-    double yh[N];
+    double e[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) yh[i] = r.b0;
+    for (int i = 0; i < N; ++i) e[i] = r.b0 - rows[i * NF + K];
 #pragma unroll
     for (int j = 0; j < K; ++j)
 #pragma unroll
-      for (int i = 0; i < N; ++i) yh[i] = fma(rows[i * NF + j], r.b[j], yh[i]);
+      for (int i = 0; i < N; ++i) e[i] = fma(rows[i * NF + j], r.b[j], e[i]);
 #pragma unroll
-    for (int i = 0; i < N; ++i) yh[i] = yh[i] - rows[i * NF + K];
-#pragma unroll
-    for (int i = 0; i < N; ++i) a[i & 3][0] = fma(yh[i], yh[i], a[i & 3][0]);
+    for (int i = 0; i < N; ++i) a[i & 3][0] = fma(e[i], e[i], a[i & 3][0]);
   }
   __device__ __forceinline__ double finish(const Reg& r, const double* acc, long n) const {
     if (n == 0) return 0.0;

@@ -71,6 +71,7 @@ struct Dev {
   int nmax;              // rows of the largest group
   int hlds, naux;        // persistent partial: Gibbs payload via LDS, auxiliary waves
   int hreg;              // persistent partial, G <= 64: Gibbs payload in registers (SYNC_REG)
+  int pair;              // persistent partial, G <= 64, P == 2: the pair kernel (pair.h)
   int noprio;            // diagnostics: no issue priority for the latency-bound waves
   int rows_lds;          // 1: each workgroup stages its group's rows in LDS once per launch
   int tile;              // target rows per likelihood tile (nmc_tiles)
@@ -124,7 +125,18 @@ struct Dev {
     if (d.stamps && blockIdx.x == 0 && w == 1 && (t) - i0 < 8 && lane == 0)              \
       d.stamps[((0 * 2 + 0) * 8 + ((t) - i0)) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// tile k of the step (t, p), workgroup 0, first 8 steps of a launch: start/end clock
+// and the wave that ran it, stamps[512 + ((step * 16 + k) * 4 + {0, 1, 2})]
+#define NMC_TILE_STAMP(k, e)                                                              \
+  do {                                                                                    \
+    const int si_ = (t - i0) * P + p;                                                     \
+    if (d.stamps && blockIdx.x == 0 && si_ < 8 && (k) < 16 && lane == 0) {               \
+      d.stamps[512 + (si_ * 16 + (k)) * 4 + (e)] = __builtin_amdgcn_s_memtime();         \
+      if (e) d.stamps[512 + (si_ * 16 + (k)) * 4 + 2] = (unsigned long long)w;           \
+    }                                                                                     \
+  } while (0)
 #else
+#define NMC_TILE_STAMP(k, e) do {} while (0)
 #define NMC_STAMP_CMP(t, slot) do {} while (0)
 #define NMC_STAMP_AUX(t, slot) do {} while (0)
 #define NMC_STAMP(t, slot) do {} while (0)
@@ -132,6 +144,8 @@ struct Dev {
 #endif
 
 enum { NMC_RUN_HYPER_LOAD = 1 };
+// Likelihood tiles per group (nmc_tiles) = partial-sum slots per accumulator.
+enum { NMC_NSLOT = 16 };
 enum { NMC_SPIN_LIMIT = 1 << 22 };
 
 // Offset of the hyper-parameter slot holding the state after iteration t ([2][P][C]:
@@ -170,7 +184,7 @@ __device__ __forceinline__ void nmc_tune(double& s, double& na, double& nr) {
 // ---------------------------------------------------------------------------
 struct nmc_lds_layout {
   int th;      // [P]            current values (control wave writes, all read)
-  int part;    // [NACC][16]     per-wave likelihood partial sums (unused slots: -0.0)
+  int part;    // [NACC][NSLOT]  per-tile likelihood partial sums (unused slots: -0.0)
   int st;      // [5][P]         scale, log prior, n acc, n rej, total acc (control wave)
   int hyp;     // [6][P]         mu, sd, log sd, sigma2, sqrt(sigma2/G), 1/sd of the hyper-prior
   int hval;    // [2][G + 1]     Gibbs payload of two tasks (persistent Gibbs-wave mode)
@@ -190,7 +204,7 @@ __host__ __device__ inline nmc_lds_layout nmc_lds(int nacc, int P, int partial, 
   nmc_lds_layout L;
   L.th = 0;
   L.part = L.th + P;
-  L.st = L.part + nacc * 16;   // 16 partial slots per accumulator (unused: -0.0)
+  L.st = L.part + nacc * NMC_NSLOT;   // partial slots per accumulator (unused: -0.0)
   L.hyp = L.st + 5 * P;
   L.hval = L.hyp + (partial ? 6 * P : 0);
   L.hst = L.hval + (partial && hlds ? 2 * (G + 1) : 0);   // two payload buffers (+1 DMA pad)
@@ -463,7 +477,7 @@ __device__ __forceinline__ void nmc_ll_rows(const Fam& fam, const typename Fam::
   for (int k = 0; k < Fam::NACC; ++k) acc[k] = (a[0][k] + a[1][k]) + (a[2][k] + a[3][k]);
 }
 
-// The regression row loop (FamLinreg<2>: rows {x, y}, e = fma(x, b1, b0) - y,
+// The regression row loop (FamLinreg<2>: rows {x, y}, e = fma(x, b1, b0 - y),
 // acc[i & 3] = fma(e, e, acc[i & 3]) for row i of each 8-row block) written by hand:
 // two fixed register sets v[192:223] / v[224:255], block b+1's eight broadcast
 // ds_read_b128 in flight while block b is consumed (counted lgkmcnt(8)).  The compiler
@@ -480,17 +494,17 @@ __device__ __forceinline__ void nmc_ll_rows(const Fam& fam, const typename Fam::
   "ds_read_b128 v[" #b "+20:" #b "+23], %[addr] offset:" #off "+80\n"      \
   "ds_read_b128 v[" #b "+24:" #b "+27], %[addr] offset:" #off "+96\n"      \
   "ds_read_b128 v[" #b "+28:" #b "+31], %[addr] offset:" #off "+112\n"
-#define NMC_E(b, k) \
-  "v_fma_f64 v[" #b "+" #k ":" #b "+" #k "+1], v[" #b "+" #k ":" #b "+" #k "+1], %[b1], %[b0]\n"
-#define NMC_D(b, k)                                                                  \
-  "v_add_f64 v[" #b "+" #k ":" #b "+" #k "+1], v[" #b "+" #k ":" #b "+" #k "+1], -v[" #b \
+#define NMC_E(b, k)                                                                  \
+  "v_fma_f64 v[" #b "+" #k ":" #b "+" #k "+1], v[" #b "+" #k ":" #b "+" #k "+1], %[b1], v[" #b \
   "+" #k "+2:" #b "+" #k "+3]\n"
+#define NMC_D(b, k)                                                                  \
+  "v_add_f64 v[" #b "+" #k "+2:" #b "+" #k "+3], %[b0], -v[" #b "+" #k "+2:" #b "+" #k "+3]\n"
 #define NMC_S(b, k, a) \
   "v_fma_f64 %[" #a "], v[" #b "+" #k ":" #b "+" #k "+1], v[" #b "+" #k ":" #b "+" #k "+1], %[" #a "]\n"
 #define NMC_B8(b)                                                                       \
-  NMC_E(b, 0) NMC_E(b, 4) NMC_E(b, 8) NMC_E(b, 12) NMC_E(b, 16) NMC_E(b, 20) NMC_E(b, 24)  \
-  NMC_E(b, 28) NMC_D(b, 0) NMC_D(b, 4) NMC_D(b, 8) NMC_D(b, 12) NMC_D(b, 16) NMC_D(b, 20)  \
-  NMC_D(b, 24) NMC_D(b, 28) NMC_S(b, 0, a0) NMC_S(b, 4, a1) NMC_S(b, 8, a2)               \
+  NMC_D(b, 0) NMC_D(b, 4) NMC_D(b, 8) NMC_D(b, 12) NMC_D(b, 16) NMC_D(b, 20) NMC_D(b, 24)  \
+  NMC_D(b, 28) NMC_E(b, 0) NMC_E(b, 4) NMC_E(b, 8) NMC_E(b, 12) NMC_E(b, 16) NMC_E(b, 20)  \
+  NMC_E(b, 24) NMC_E(b, 28) NMC_S(b, 0, a0) NMC_S(b, 4, a1) NMC_S(b, 8, a2)               \
   NMC_S(b, 12, a3) NMC_S(b, 16, a0) NMC_S(b, 20, a1) NMC_S(b, 24, a2) NMC_S(b, 28, a3)
 typedef __attribute__((address_space(3))) const double* nmc_lds_cptr;
 __device__ __forceinline__ void nmc_rows_lds_linreg2(const double* p, int nb, double b0,
@@ -593,6 +607,19 @@ __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename F
   for (int k = 0; k < Fam::NACC; ++k) acc[k] = (a[0][k] + a[1][k]) + (a[2][k] + a[3][k]);
 }
 
+// The tile partials of one sum in a fixed order: tile k into accumulator k % 4, combined
+// (a0+a1)+(a2+a3); every LDS read in flight at once (slots past the last tile hold -0.0,
+// and x + (-0.0) == x).
+__device__ __forceinline__ double nmc_sum_slots(const double* pt) {
+  double v[NMC_NSLOT];
+#pragma unroll
+  for (int u = 0; u < NMC_NSLOT; ++u) v[u] = pt[u * 64];
+  double a4[4];
+#pragma unroll
+  for (int u = 0; u < NMC_NSLOT; ++u) a4[u & 3] = u < 4 ? v[u] : a4[u & 3] + v[u];
+  return (a4[0] + a4[1]) + (a4[2] + a4[3]);
+}
+
 // Chunk k of nchunks of [r0, r1) (contiguous, balanced).
 __device__ __forceinline__ void nmc_chunk(int64_t r0, int64_t r1, int k, int nchunks,
                                           int64_t* a, int* n) {
@@ -618,25 +645,41 @@ __device__ __forceinline__ void nmc_load_theta(const Dev& d, const double* src, 
 }
 
 // ---------------------------------------------------------------------------
-// Row tiles of one group (the likelihood partition): NT = min(16, ceil(n/tile)) tiles
-// (tile = 64 rows unless a diagnostics override sets it)
-// of TL rows (a multiple of 16, so every tile but the last runs whole 16-row blocks
-// of the pipelined loop), the last tile taking the rest.  Depends only on the group's
-// row count: the tile partials -- and so every log-likelihood sum -- are the same
-// whichever wave computes a tile, whatever the chain count, launch mode or GPU count.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void nmc_tiles(int n, int tile, int* nt, int* tl) {
+// Row tiles of one group (the likelihood partition): NT = min(NSLOT, ceil(n/tile)) tiles
+// (tile = 64 rows unless a diagnostics override sets it) of a multiple of 16 rows, so
+// every tile but the last runs whole 16-row blocks of the pipelined loop.  Depends only
+// on the group's row count: the tile partials -- and so every log-likelihood sum -- are
+// the same whichever wave computes a tile, whatever the chain count, launch mode or GPU
+// count.  Tile k covers [start(k), start(k) + len(k)).  (A two-length partition -- the
+// first half of the tiles carrying 5/8 of the rows -- measured 9.6 against 8.4 us per
+// iteration at cfg 3: the late tiles were not the tail.)
+struct nmc_tiling {
+  int nt;     // tiles
+  int h;      // tiles [0, h) have a rows, [h, nt) b rows (the last one the remainder)
+  int a, b;
+  int n;
+  __device__ __forceinline__ int start(int k) const { return k < h ? k * a : h * a + (k - h) * b; }
+  __device__ __forceinline__ int len(int k) const {
+    const int s = start(k);
+    const int e = s + (k < h ? a : b);
+    return (e < n ? e : n) - s;
+  }
+};
+__device__ __forceinline__ nmc_tiling nmc_tiles(int n, int tile) {
+  nmc_tiling T;
+  T.n = n > 0 ? n : 0;
   if (n <= 0) {
-    *nt = 1;
-    *tl = 0;
-    return;
+    T.nt = 1; T.h = 1; T.a = T.b = 0;
+    return T;
   }
   int t = (n + tile - 1) / tile;
-  if (t > 16) t = 16;
+  if (t > NMC_NSLOT) t = NMC_NSLOT;
   int per = (n + t - 1) / t;
   per = (per + 15) & ~15;
-  *tl = per;
-  *nt = (n + per - 1) / per;
+  T.a = T.b = per;
+  T.nt = (n + per - 1) / per;
+  T.h = T.nt;
+  return T;
 }
 
 // Groups [kb, ke) of the chain block's published values of parameter p (64 chains
@@ -818,14 +861,15 @@ __device__ __forceinline__ double nmc_pairwise_reg(const double (&x)[64], int G,
 // The Gibbs update of parameter p after iteration t for this wave's 64 chains from the
 // chain block's values x[0..G) of p in registers (G <= 64); otherwise identical to
 // nmc_hyper_compute (same sums in the same order, same draws, same outputs).
+// hyp: the LDS column of the hyper state ([6][P] columns, NMC_HY_*).
 __device__ __forceinline__ void nmc_hyper_compute_reg(const Dev& d, int cb, int t, int p,
-                                                      double* lds, const nmc_lds_layout& L,
-                                                      bool write, double hz, double hx,
+                                                      double* lds, int hyp, bool write,
+                                                      double hz, double hx,
                                                       const double (&x)[64]) {
   const int lane = threadIdx.x & 63;
   const int P = d.P, G = d.G, C = d.C;
   const int c = cb * 64 + lane;
-  double* hy = lds + L.hyp * 64 + lane;
+  double* hy = lds + hyp * 64 + lane;
   const double sdm = sqrt(hy[(NMC_HY_S2 * P + p) * 64] / G);
   const double tot = nmc_pairwise_reg(x, G, false, 0.0);
   const double mu = tot / G + sdm * hz;                        // mu ~ N(mean(x), sqrt(s2/G))
@@ -885,7 +929,7 @@ __device__ __forceinline__ void nmc_hyper_fetch_reg(const Dev& d, int tq, int q,
 //   every wave        once its own work is done, takes likelihood row tiles from an
 //                     LDS counter until none is left, so a wave that shares its SIMD
 //                     with a busy control or Gibbs wave simply takes fewer tiles.
-// The control wave adds the 16 tile partials in a fixed order (nmc_tiles): the sums do
+// The control wave adds the tile partials in a fixed order (nmc_tiles): the sums do
 // not depend on which wave took which tile.
 //   flags & NMC_RUN_HYPER_LOAD: the hyper-parameters after iteration i0-1 are in
 //     global memory (chunk start / initial state); otherwise (launch per iteration)
@@ -899,8 +943,10 @@ enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
        NMC_MODE_LAUNCH = 1,      // one launch per iteration, plain loads after the boundary
        NMC_MODE_SYNC = 2,        // persistent, sc1 loads after the barrier
        NMC_MODE_SYNC_LDS = 3,    // persistent, the Gibbs wave works on an LDS copy
-       NMC_MODE_SYNC_REG = 4 };  // persistent, G <= 64: the Gibbs wave fetches the task's
+       NMC_MODE_SYNC_REG = 4,    // persistent, G <= 64: the Gibbs wave fetches the task's
                                  // values straight into registers and updates in one step
+       NMC_MODE_PAIR = 5 };      // persistent, G <= 64, P == 2: both steps of an iteration
+                                 // from one pass over the rows (pair.h, nmc_k_pair)
 template <class Fam, int MODE>
 __global__ void __launch_bounds__(512)
 nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int flags) {
@@ -935,8 +981,8 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   unsigned* tcnt = (unsigned*)(lds + L.flag * 64 + 4);
   const int64_t r0 = d.off[g];
   const int nrow = (int)(d.off[g + 1] - r0);
-  int nt, tl;
-  nmc_tiles(nrow, d.tile, &nt, &tl);
+  const nmc_tiling TI = nmc_tiles(nrow, d.tile);
+  const int nt = TI.nt;
   const double* grows = obs + r0 * Fam::NFIELDS;
   const size_t PGC = (size_t)P * G * C;
   const size_t gc = (size_t)g * C + cc;
@@ -982,8 +1028,8 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   double* cwv = lds + L.cw * 64 + lane;    // cwv[k * 64]: control-wave values across barriers
   if (ctl) {     // {z, log u} of the first step -> LDS slot of step i0*P
     nmc_dma16(zl_src(i0, 0), lds + (L.zl + 2 * ((i0 * P) & 1)) * 64);
-    for (int j = 0; j < Fam::NACC; ++j)   // x + (-0.0) == x: the fixed 16-slot sum
-      for (int k = nt; k < 16; ++k) lds[(L.part + j * 16 + k) * 64 + lane] = -0.0;
+    for (int j = 0; j < Fam::NACC; ++j)   // x + (-0.0) == x: the fixed slot sum
+      for (int k = nt; k < NMC_NSLOT; ++k) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = -0.0;
     nmc_drain_vm();
     lds[L.flag * 64 + lane] = 0.0;       // (also zeroes both tile counters)
   }
@@ -1050,7 +1096,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             nmc_drain_vm();
             if (p == 0) NMC_STAMP_AUX(t, 14);
 #endif
-            nmc_hyper_compute_reg(d, cb, kt, kq, lds, L, g == 0, fz, fx, xv);
+            nmc_hyper_compute_reg(d, cb, kt, kq, lds, L.hyp, g == 0, fz, fx, xv);
             if (p == 0) NMC_STAMP_AUX(t, 15);
             if (P <= 2) {   // the update lands in the step that needs it: this step's priors
               const int sp = gs & 1;
@@ -1081,7 +1127,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         for (int k = ge - lag > gs0 ? ge - lag : gs0; k < ge; ++k) {
           double xv[64], fz, fx;
           nmc_hyper_fetch_reg(d, k / P, k % P, cc, xv, fz, fx);
-          nmc_hyper_compute_reg(d, cb, k / P, k % P, lds, L, true, fz, fx, xv);
+          nmc_hyper_compute_reg(d, cb, k / P, k % P, lds, L.hyp, true, fz, fx, xv);
         }
       }
     }
@@ -1166,8 +1212,8 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       //      task gs-1, the pending state update, both outcomes of the decision --
       //      accept (sA, naA, nrA, ta + 1) / reject (sR, naR, nrR, ta), tuned if due --,
       //      the next step's variates in flight, priors ----
-      if (ctl) {
-        if constexpr (sync) {   // the previous step's value is stored; count it published
+      auto ctl_work = [&]() {
+        if constexpr (sync && !hr) {   // the previous step's value is stored; count it published
           if (pub_p >= 0) {
             nmc_drain_vm();
             if (lane == 0)
@@ -1212,9 +1258,6 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
           cwv[NMC_CW_NRR * 64] = nrR;
           cwv[NMC_CW_TA * 64] = st[(NMC_ST_TA * P + p) * 64];
         }
-        const int tn = p + 1 < P ? t : t + 1;
-        const int pn = p + 1 < P ? p + 1 : 0;
-        if (tn < i1) nmc_dma16(zl_src(tn, pn), lds + (L.zl + 2 * (sp ^ 1)) * 64);
         if (!hl && hyper_now) nmc_hyper_variates(d, cb, t - 1, lds, L, 0, 1);
         if (PARTIAL && !hl && p == (P > 1 ? 1 : 0)) nmc_hyper_sdm(d, lds, L, lane);
         if (!hyper_now && !(hl && post_prior)) {   // priors (:293-294)
@@ -1228,6 +1271,24 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             c_lpp = nmc_prior_logpdf(d.pfam[p], d.ppar + 8 * p, c_prop);
           }
         }
+        if constexpr (hr) {   // count the previous step's value published: its store has had
+                              // the pre-work above to drain (the Gibbs waves poll two steps on)
+          if (pub_p >= 0) {
+            nmc_drain_vm();
+            if (lane == 0)
+              __hip_atomic_fetch_add(nmc_counter(d, cb, pub_p, g & 7), 1u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+            pub_p = -1;
+          }
+        }
+        const int tn = p + 1 < P ? t : t + 1;
+        const int pn = p + 1 < P ? p + 1 : 0;
+        if (tn < i1) nmc_dma16(zl_src(tn, pn), lds + (L.zl + 2 * (sp ^ 1)) * 64);
+            };
+      bool ctl_done = !ctl;
+      if (ctl) {
+        ctl_work();
+        ctl_done = true;
       }
       // ---- likelihood of the proposal (:615-635), tile by tile, every wave ----
       {
@@ -1251,16 +1312,26 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         int k = (int)__builtin_amdgcn_readlane(grab(), 0);
         while (k < nt) {
           const unsigned kn = grab();
-          const int ra = k * tl;
-          const int rn = (k + 1 == nt ? nrow : ra + tl) - ra;
+          const int ra = TI.start(k);
+          const int rn = TI.len(k);
+          NMC_TILE_STAMP(k, 0);
           double acc[Fam::NACC];
           if (d.rows_lds)   // wave-uniform LDS address: broadcast ds_reads, software-pipelined
             nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
           else              // wave-uniform global address: scalar loads
             nmc_ll_rows(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, acc);
 #pragma unroll
-          for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * 16 + k) * 64 + lane] = acc[j];
+          for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = acc[j];
+          NMC_TILE_STAMP(k, 1);
+          if (!ctl_done) {
+            ctl_work();
+            ctl_done = true;
+          }
           k = (int)__builtin_amdgcn_readlane(kn, 0);
+        }
+        if (!ctl_done) {   // (no tile left for the control wave)
+          ctl_work();
+          ctl_done = true;
         }
       }
       NMC_STAMP(t, 1 + 3 * (p & 1));
@@ -1269,12 +1340,11 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       NMC_STAMP(t, 2 + 3 * (p & 1));
 
       // ---- Gibbs update after iteration t-1 (needed by this iteration's priors) ----
-      if constexpr (hl) {
-        if (aux_now) {   // the poller's verdict
-          ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
-          if (!ok) break;
-        }
-      }
+      // (Gibbs-wave modes: the poller's verdict is read in the same LDS batch as the
+      // decision's operands and checked after the decision; an aborted step's decision is
+      // never used -- the launch reports the timeout)
+      double verdict = 0.0;
+      if constexpr (hl) if (aux_now) verdict = lds[L.flag * 64 + 1];
       if constexpr (PARTIAL && !hl) if (hyper_now) {
         if constexpr (sync) {   // every parameter of t-1 is published once P-1's count is full
           ok = nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(t - i0), lds, L);
@@ -1299,18 +1369,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         double acc[Fam::NACC];
 #pragma unroll
         for (int j = 0; j < Fam::NACC; ++j) {
-          // the tile partials in a fixed order: tile k into accumulator k % 4, combined
-          // (a0+a1)+(a2+a3); every LDS read in flight at once (slots past the last tile
-          // hold -0.0)
-          const double* pt = lds + (L.part + j * 16) * 64 + lane;
-          double a4[4] = {0.0, 0.0, 0.0, 0.0};
-          double v16[16];
-#pragma unroll
-          for (int u = 0; u < 16; ++u) v16[u] = pt[u * 64];
-#pragma unroll
-          for (int u = 0; u < 16; ++u)
-            a4[u & 3] = u < 4 ? v16[u] : a4[u & 3] + v16[u];
-          acc[j] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+          acc[j] = nmc_sum_slots(lds + (L.part + j * NMC_NSLOT) * 64 + lane);
         }
         if (p == 0) NMC_STAMP(t, 10);
         double thp[Fam::MAXP];
@@ -1348,6 +1407,10 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         pend_t = t;
         // the rest of the update waits for the next step's pre-barrier slack
         if (p == 0) NMC_STAMP(t, 12);
+      }
+      if constexpr (hl) if (aux_now) {
+        ok = verdict == 2.0 * ((double)gs + 1);
+        if (!ok) break;
       }
       if (p == 0) NMC_STAMP(t, 3);
       __syncthreads();      // the new value is visible to every wave

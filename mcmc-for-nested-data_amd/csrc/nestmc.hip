@@ -83,6 +83,15 @@ static void choose_geometry(nmc_ctx* x) {
   // G <= 64: the Gibbs wave fetches a task's values into registers (one sc1 round trip)
   // and updates in the step after publication (no LDS payload, no two-stage pipeline)
   d.hreg = d.hlds && d.G <= 64 && !(getenv("NMC_NO_HREG") && atoi(getenv("NMC_NO_HREG")));
+  // P == 2 with rows in LDS: both steps of an iteration from one pass (pair.h); needs
+  // the control wave, two Gibbs waves and at least one likelihood wave
+  // (measured on MI355X at cfg 3: 8.6-9.8 us per iteration against 8.0 for SYNC_REG --
+  // the three-sum pass is VALU-bound with two of the four SIMDs holding a Gibbs wave --
+  // so it is opt-in, NMC_PAIR=1, for the measurements in DESIGN.md)
+  d.pair = d.hreg && d.P == 2 && d.rows_lds &&
+           (size_t)nmc_pair_lds(x->nacc, d.nmax * x->nf).total * 512 <= (size_t)160 * 1024 &&
+           getenv("NMC_PAIR") && atoi(getenv("NMC_PAIR"));
+  if (d.pair && d.W < 4) d.W = 4;
 }
 
 // numpy's pairwise-sum recursion over G groups (numpy/_core/src/umath/loops_utils.h):
@@ -760,12 +769,12 @@ int nmc_debug_stamps(nmc_ctx* x, int n, uint64_t* out) {
   hipSetDevice(x->device);
   if (n > 0) {
     if (!x->d.stamps)
-      if (int rc = dalloc(x, &x->d.stamps, 512)) return rc;
-    HIPCHK(hipMemset(x->d.stamps, 0, 512 * 8));
+      if (int rc = dalloc(x, &x->d.stamps, 1024)) return rc;
+    HIPCHK(hipMemset(x->d.stamps, 0, 1024 * 8));
   }
-  if (out) {
+  if (out) {   // [0, 512): phase stamps; [512, 1024): tile stamps (nmc_k_run)
     HIPCHK(hipStreamSynchronize(x->stream));
-    HIPCHK(hipMemcpy(out, x->d.stamps, 512 * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out, x->d.stamps, 1024 * 8, hipMemcpyDeviceToHost));
   }
   return 0;
 #else
