@@ -110,6 +110,15 @@ int nmc_eval_group_ll(nmc_ctx* ctx, const double* theta, double* out);
 /* StepMethod.logLikelihood (:656-659): per-observation LL at the current state,
  * out[C][n_obs] (saveLogLikelihood rows, :907-909).                          */
 int nmc_eval_obs_ll(nmc_ctx* ctx, double* out);
+/* The same at recorded rows [row_begin, row_begin+n_rows) of the sample store -- the
+ * state Sampler._printLogLikelihood (:890-891) evaluated at each recorded iteration:
+ * out[C][n_rows][n_obs].                                                       */
+int nmc_obs_ll_rows(nmc_ctx* ctx, int row_begin, int n_rows, double* out);
+/* saveLogLikelihood=True (:890-891, :907-909): logLikelihood.<chain_ids[c]>.csv in dir
+ * (a path prefix ending in '/') for every local chain and recorded row, "%f" joined by
+ * ",".  Batches of rows are evaluated on the device and copied to pinned memory while
+ * the host formats the previous batch with `threads` threads.                  */
+int nmc_write_ll_csvs(nmc_ctx* ctx, const char* dir, const int32_t* chain_ids, int threads);
 
 /* Timing on the context's stream (hipEvents). */
 int nmc_event_record(nmc_ctx* ctx, int slot);                 /* slot 0..15 */

@@ -52,6 +52,7 @@ struct nmc_ctx {
   int nacc = 1;                           // likelihood accumulators of the family
   bool persistent = false;                // partial pooling: one resident launch per chunk
   int ncu = 256;
+  int* gidx = nullptr;                    // [n_obs] group of each observation (obs-LL rows)
 };
 
 static inline double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->d.vb0; }
@@ -99,7 +100,8 @@ enum {
   NMC_OP_RUN = 0,          // step kernel over iterations [i0, i1) with flags
   NMC_OP_CAN_PERSIST = 1,  // result = 1 if the persistent grid is co-resident
   NMC_OP_GROUP_LL = 2,     // in = theta [P][G][C] (device), out = [G][C] (device)
-  NMC_OP_OBS_LL = 3        // in = values [P][G][C] (device), out = [C][n_obs] (device)
+  NMC_OP_OBS_LL = 3,       // in = values [P][G][C] (device), out = [C][n_obs] (device)
+  NMC_OP_OBS_LL_ROWS = 4   // sample rows [i0, i1) -> out = [C][i1 - i0][n_obs] (device)
 };
 struct NmcCall {
   int op = 0;

@@ -12,10 +12,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <charconv>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
-#include <algorithm>
 
 #include "ctx.h"
 #include "kernels_misc.h"
@@ -630,17 +632,18 @@ int nmc_launch_config(nmc_ctx* x, int* waves_per_group, int* chain_blocks, int* 
 // CSV output with the reference's formatting (Python "%f" == C "%f" except the
 // spelling of NaN, which Python always prints as "nan").
 // ---------------------------------------------------------------------------
+// std::to_chars(fixed, 6) is the exact decimal "%f" produces (both correctly rounded),
+// at several times snprintf's speed; 512 bytes hold any finite double's fixed form.
 static inline void put_f(std::string& s, double v) {
   char buf[512];
   if (isnan(v)) { s += "nan"; return; }
   if (isinf(v)) { s += v > 0 ? "inf" : "-inf"; return; }
-  int n = snprintf(buf, sizeof(buf), "%f", v);
-  if (n >= (int)sizeof(buf)) {
-    std::vector<char> big(n + 1);
-    snprintf(big.data(), big.size(), "%f", v);
-    s += big.data();
+  const std::to_chars_result r = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::fixed, 6);
+  if (r.ec == std::errc()) {
+    s.append(buf, r.ptr - buf);
   } else {
-    s.append(buf, n);
+    const int n = snprintf(buf, sizeof(buf), "%f", v);
+    s.append(buf, n < (int)sizeof(buf) ? n : (int)sizeof(buf) - 1);
   }
 }
 
@@ -666,6 +669,132 @@ int nmc_write_sample_csv(const char* path, int append, const char* header, const
   fclose(f);
   if (w != s.size()) return fail(-3, std::string("short write to ") + path);
   return 0;
+}
+
+// the group of every observation (CSR order), built once per context
+static int ensure_gidx(nmc_ctx* x) {
+  if (x->gidx || x->n_obs == 0) return 0;
+  std::vector<int64_t> off(x->G + 1);
+  HIPCHK(hipMemcpy(off.data(), x->d.off, (x->G + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+  std::vector<int> gi(x->n_obs);
+  for (int g = 0; g < x->G; ++g)
+    for (int64_t i = off[g]; i < off[g + 1]; ++i) gi[i] = g;
+  if (int rc = dalloc(x, &x->gidx, (size_t)x->n_obs)) return rc;
+  HIPCHK(hipMemcpy(x->gidx, gi.data(), x->n_obs * sizeof(int), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int nmc_obs_ll_rows(nmc_ctx* x, int row_begin, int n_rows, double* out) {
+  hipSetDevice(x->device);
+  if (row_begin < 0 || n_rows < 0 || row_begin + n_rows > x->d.n_rows || n_rows > 65535)
+    return fail(-1, "row range out of bounds (at most 65535 rows per call)");
+  HIPCHK(hipStreamSynchronize(x->stream));
+  if (int rc = check_timeout(x)) return rc;
+  if (int rc = ensure_gidx(x)) return rc;
+  const size_t n = (size_t)x->C * n_rows * x->n_obs;
+  if (n == 0) return 0;
+  double* o = nullptr;
+  HIPCHK(hipMalloc(&o, n * 8));
+  NmcCall c;
+  c.op = NMC_OP_OBS_LL_ROWS;
+  c.i0 = row_begin;
+  c.i1 = row_begin + n_rows;
+  c.out = o;
+  int rc = nmc_call_family(x, c);
+  if (!rc) {
+    hipError_t e = hipMemcpyAsync(out, o, n * 8, hipMemcpyDeviceToHost, x->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(x->stream);
+    if (e != hipSuccess) rc = fail(-2, std::string("obs_ll_rows: ") + hipGetErrorString(e));
+  }
+  hipFree(o);
+  return rc;
+}
+
+// saveLogLikelihood (Sampler._printLogLikelihood :907-909 at every recorded row, the LL
+// of :656-659 evaluated at the recorded values): batches of rows are evaluated on the
+// device into one of two buffers and copied to pinned host memory while the host
+// formats and appends the previous batch, one thread per group of chain files.
+int nmc_write_ll_csvs(nmc_ctx* x, const char* dir, const int32_t* chain_ids, int threads) {
+  hipSetDevice(x->device);
+  HIPCHK(hipStreamSynchronize(x->stream));
+  if (int rc = check_timeout(x)) return rc;
+  const int rows = x->d.n_rows;
+  const int C = x->C;
+  const int64_t n_obs = x->n_obs;
+  if (rows == 0 || n_obs == 0) return 0;
+  if (int rc = ensure_gidx(x)) return rc;
+  const size_t per_row = (size_t)C * n_obs * 8;
+  int nb = (int)std::max<size_t>(1, ((size_t)256 << 20) / per_row);
+  nb = std::min(nb, std::min(rows, 65535));
+  const int nbatch = (rows + nb - 1) / nb;
+  double* dbuf[2] = {nullptr, nullptr};
+  double* hbuf[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int rc = 0;
+  auto cleanup = [&]() {
+    for (int i = 0; i < 2; ++i) {
+      if (dbuf[i]) hipFree(dbuf[i]);
+      if (hbuf[i]) hipHostFree(hbuf[i]);
+      if (ev[i]) hipEventDestroy(ev[i]);
+    }
+  };
+  for (int i = 0; i < 2 && !rc; ++i) {
+    if (hipMalloc(&dbuf[i], nb * per_row) != hipSuccess ||
+        hipHostMalloc(&hbuf[i], nb * per_row, hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
+      rc = fail(-2, "write_ll_csvs: out of device or pinned host memory");
+  }
+  auto launch = [&](int b) -> int {
+    const int r0 = b * nb, n = std::min(nb, rows - r0);
+    NmcCall c;
+    c.op = NMC_OP_OBS_LL_ROWS;
+    c.i0 = r0;
+    c.i1 = r0 + n;
+    c.out = dbuf[b & 1];
+    if (int e = nmc_call_family(x, c)) return e;
+    HIPCHK(hipMemcpyAsync(hbuf[b & 1], dbuf[b & 1], n * per_row, hipMemcpyDeviceToHost, x->stream));
+    HIPCHK(hipEventRecord(ev[b & 1], x->stream));
+    return 0;
+  };
+  const int T = std::max(1, std::min(threads, C));
+  if (!rc) rc = launch(0);
+  for (int b = 0; b < nbatch && !rc; ++b) {
+    if (b + 1 < nbatch && (rc = launch(b + 1))) break;
+    if (hipEventSynchronize(ev[b & 1]) != hipSuccess) { rc = fail(-2, "write_ll_csvs: device"); break; }
+    const int n = std::min(nb, rows - b * nb);
+    const double* hb = hbuf[b & 1];
+    std::vector<std::string> errs(T);
+    auto work = [&](int tid) {
+      std::string s;
+      for (int c = tid; c < C; c += T) {
+        char path[4096];
+        snprintf(path, sizeof(path), "%slogLikelihood.%d.csv", dir, chain_ids[c]);
+        FILE* f = fopen(path, b == 0 ? "w" : "a");
+        if (!f) { errs[tid] = std::string("cannot open ") + path; return; }
+        s.clear();
+        for (int r = 0; r < n; ++r) {
+          const double* v = hb + ((size_t)c * n + r) * n_obs;
+          for (int64_t i = 0; i < n_obs; ++i) {
+            if (i) s += ',';
+            put_f(s, v[i]);
+          }
+          s += '\n';
+          if (s.size() > (1u << 22)) { fwrite(s.data(), 1, s.size(), f); s.clear(); }
+        }
+        const size_t w = fwrite(s.data(), 1, s.size(), f);
+        if (fclose(f) != 0 || w != s.size()) { errs[tid] = std::string("short write to ") + path; return; }
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int tid = 1; tid < T; ++tid) pool.emplace_back(work, tid);
+    work(0);
+    for (auto& th : pool) th.join();
+    for (auto& e : errs)
+      if (!e.empty()) { rc = fail(-3, e); break; }
+  }
+  if (rc) hipStreamSynchronize(x->stream);
+  cleanup();
+  return rc;
 }
 
 int nmc_write_ll_csv(const char* path, int append, const double* ll, int64_t n, int n_rows) {

@@ -206,6 +206,7 @@ nmc_k_pair(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int G = d.G, C = d.C;
   const int W = blockDim.x >> 6;   // (diagnostic stamps)
+  (void)W;
   const int b = blockIdx.x;
   const int g = b % G, cb = b / G;
   const int c = cb * 64 + lane;

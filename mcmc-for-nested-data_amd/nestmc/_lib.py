@@ -55,6 +55,8 @@ SIGNATURES = {
     "nmc_get_accept_counts": (ctypes.c_int, [_vp, _c_int64_p]),
     "nmc_eval_group_ll": (ctypes.c_int, [_vp, _c_double_p, _c_double_p]),
     "nmc_eval_obs_ll": (ctypes.c_int, [_vp, _c_double_p]),
+    "nmc_obs_ll_rows": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _c_double_p]),
+    "nmc_write_ll_csvs": (ctypes.c_int, [_vp, ctypes.c_char_p, _c_int32_p, ctypes.c_int]),
     "nmc_event_record": (ctypes.c_int, [_vp, ctypes.c_int]),
     "nmc_event_elapsed": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_float)]),

@@ -159,6 +159,24 @@ class Engine:
         check(self.lib.nmc_eval_group_ll(self.h, dptr(th), dptr(out)))
         return out.T.copy()
 
+    def obs_ll_rows(self, row_begin=0, n_rows=None):
+        """Per-observation LL at recorded rows of the sample store: [C, rows, n_obs]."""
+        if n_rows is None:
+            n_rows = self.n_rows - row_begin
+        out = numpy.empty((self.C, n_rows, int(self.off[-1])))
+        check(self.lib.nmc_obs_ll_rows(self.h, row_begin, n_rows, dptr(out)))
+        return out
+
+    def write_ll_csvs(self, sample_dir, chain_ids, threads=8):
+        """logLikelihood.<id>.csv for every local chain and recorded row (streamed)."""
+        ids = numpy.ascontiguousarray(chain_ids, dtype=numpy.int32)
+        if len(ids) != self.C:
+            raise ValueError("need one file id per local chain")
+        d = sample_dir if sample_dir.endswith("/") else sample_dir + "/"
+        check(self.lib.nmc_write_ll_csvs(self.h, d.encode(),
+                                         ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                         int(threads)))
+
     def eval_obs_ll(self):
         """Per-observation LL at the current state: [C, n_obs]."""
         out = numpy.empty((self.C, int(self.off[-1])))

@@ -164,31 +164,23 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
     if displayProgress:
         output.print_progress("Sampling started. 0% complete.")
     t_loop = datetime.datetime.now()
-    if saveLogLikelihood and write_files:
-        # per recorded row: advance to it, evaluate every observation's LL (:656-659)
-        prev = 0
-        for i in rec:
-            for eng, _, _ in engines:
-                eng.run(prev, i + 1)
-            for eng, _, ids in engines:
-                ll = eng.eval_obs_ll()
-                output.append_ll_rows(sample_dir, ll[:, None, :], ids)
-            prev = i + 1
+    steps = 10 if displayProgress and nIter >= 10 else 1
+    bounds = [round(nIter * k / steps) for k in range(steps + 1)]
+    for k in range(steps):
         for eng, _, _ in engines:
-            eng.run(prev, nIter)
-    else:
-        steps = 10 if displayProgress and nIter >= 10 else 1
-        bounds = [round(nIter * k / steps) for k in range(steps + 1)]
-        for k in range(steps):
+            eng.run(bounds[k], bounds[k + 1])
+        if displayProgress and steps > 1:
             for eng, _, _ in engines:
-                eng.run(bounds[k], bounds[k + 1])
-            if displayProgress and steps > 1:
-                for eng, _, _ in engines:
-                    eng.synchronize()
-                output.print_progress("%i%% complete." % (100 * (k + 1) // steps))
+                eng.synchronize()
+            output.print_progress("%i%% complete." % (100 * (k + 1) // steps))
     for eng, _, _ in engines:
         eng.synchronize()
     loop_seconds = (datetime.datetime.now() - t_loop).total_seconds()
+    if saveLogLikelihood and write_files:
+        # every recorded row's per-observation LL (:890-891, :907-909 at the values of
+        # :656-659), re-evaluated on the device from the sample store and streamed out
+        for eng, _, ids in engines:
+            eng.write_ll_csvs(sample_dir, ids, threads=threads)
 
     # ---- samples -> files ----------------------------------------------------
     header = output.header_names(names, G, partial)
