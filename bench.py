@@ -67,14 +67,12 @@ def make_engine(args, rank, device):
     fam = LinearRegression.simple(x, y, sigma=1.0)
     sizes = [N] * G
     chains = range(rank * C, (rank + 1) * C)
-    # reference-exact host init (start point uniform in the example ranges) on a
-    # few chains, replicated: init is outside the timed region and not the workload
-    st = init_chains(fam, sizes, ("b0", "b1"), chains[:8], "partial", None,
-                     {"b0": [-1, 1], "b1": [0, 3]}, False, threads=8)
-    rep = lambda a: numpy.concatenate([a] * (C // 8 + 1))[:C]   # noqa: E731
     eng = Engine(fam, sizes, C, "partial", seed=1234, chain_base=rank * C, device=device)
-    eng.set_state(rep(st["value"]), rep(st["log_prior"]), rep(st["ll"]), rep(st["mu"]),
-                  rep(st["s2"]))
+    # reference-order init of every chain (start point uniform in the example ranges),
+    # likelihoods batched on the device; outside the timed region
+    st = init_chains(fam, sizes, ("b0", "b1"), chains, "partial", None,
+                     {"b0": [-1, 1], "b1": [0, 3]}, False, group_ll=eng.eval_group_ll)
+    eng.set_state(st["value"], st["log_prior"], st["ll"], st["mu"], st["s2"])
     return eng, fam
 
 

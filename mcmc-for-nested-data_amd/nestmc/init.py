@@ -1,4 +1,4 @@
-"""Host-side chain initialisation, reproducing the reference's RNG consumption.
+"""Chain initialisation, reproducing the reference's RNG consumption, batched over chains.
 
 Chain c is seeded with ``RandomState(c)`` exactly like ``numpy.random.seed(chain)``
 (posteriorSampling.py:225, :1015), so the start values equal the reference's:
@@ -14,7 +14,16 @@ Chain c is seeded with ``RandomState(c)`` exactly like ``numpy.random.seed(chain
                 _determineIndividualStartingPoint (:746-758), including the stale
                 logPrior of re-drawn groups (:284-285).
 
-This is one-off host work, not the sampling hot loop.
+Every chain draws from its own RandomState, so the chains can advance in lock step:
+each round of the start-point search and of the partial init loop evaluates the
+likelihoods of ALL chains in one batched call -- ``group_ll(theta[C, P, G]) -> [C, G]``,
+the device's nmc_eval_group_ll -- and only the chains whose result
+was not finite draw again, in the reference's order.  The draws and the decisions
+taken on them are the reference's; only the finiteness tests and the stored group
+log-likelihoods come from the device (its summation order; the first accepted step
+replaces the latter anyway).  The MLE objective stays the exact numpy sum of the
+family callable (:1102-1105): its value steers Nelder-Mead, so it keeps the
+reference's rounding.  Without ``group_ll`` the host evaluates the family callable.
 """
 
 import warnings
@@ -46,6 +55,18 @@ def _norm_logpdf(x, loc, scale):
     if not scale > 0 or numpy.isnan(y):
         return numpy.nan
     return float(out)
+
+
+def _norm_logpdf_groups(x, loc, scale):
+    """_norm_logpdf over one parameter's G values (elementwise the same IEEE operations;
+    the one log is of the scalar scale, as in the scalar form)."""
+    if not scale > 0:
+        return numpy.full(x.shape, numpy.nan)
+    with numpy.errstate(divide="ignore", invalid="ignore"):
+        y = (x - loc) / scale
+        out = (-y ** 2 / 2.0 - LOG_C) - numpy.log(scale)
+    out[numpy.isnan(y)] = numpy.nan
+    return out
 
 
 def group_sums(ll, off):
@@ -113,67 +134,142 @@ def find_starting_point(family, n_total, names, rs, priors, ranges, mle):
     return start
 
 
-def init_chain(family, sizes, names, chain, pooling, priors, ranges, mle, group_ll=None):
-    """Initial state of global chain ``chain`` (sizes already pooled for 'complete')."""
+def _draw_start(names, rs, priors, ranges):
+    """One start candidate x[P] of MCMC._findStartingPoint (:1070-1079)."""
+    x = [0] * len(names)
+    for i, name in enumerate(names):
+        if name in ranges:
+            x[i] = rs.uniform(low=ranges[name][0], high=ranges[name][1])
+        elif priors is not None:
+            x[i] = priors[i].rvs(random_state=rs)
+        else:
+            raise ValueError(
+                "parameter %r needs a startingPointValueRange entry or a prior "
+                "(the reference fails here with numpy.random.norm, :1079)" % name)
+    return x
+
+
+def _host_batch_group_ll(family, sizes, off):
+    one = host_group_ll(family, sizes, off)
+
+    def f(theta):
+        return numpy.stack([one(theta[c]) for c in range(theta.shape[0])])
+    return f
+
+
+def init_chains(family, sizes, names, chains, pooling, priors, ranges, mle, threads=1,
+                group_ll=None):
+    """Stacked initial states for global chain ids ``chains``: dict of [C, ...] arrays.
+
+    group_ll: batched group log-likelihoods theta[C, P, G] -> [C, G] for exactly these
+    chains (the device's Engine.eval_group_ll); None evaluates the family on the host.
+    """
+    chains = [int(c) for c in chains]
+    C, P, G = len(chains), len(names), len(sizes)
     sizes = numpy.asarray(sizes, dtype=numpy.int64)
     off = numpy.concatenate([[0], numpy.cumsum(sizes)])
     n_total = int(off[-1])
-    rs = numpy.random.RandomState(chain)
-    start = find_starting_point(family, n_total, names, rs, priors, ranges, mle)
-    P, G = len(names), len(sizes)
-    if pooling in ("none", "complete"):
-        value = numpy.array([[float(start[p])] * G for p in range(P)])
-        lp = numpy.array([[float(priors[p].logpdf(start[p]))] * G for p in range(P)])
-        return ChainInit(value, lp, numpy.full(G, numpy.nan))
+    ranges = ranges or {}
     if group_ll is None:
-        group_ll = host_group_ll(family, sizes, off)
-    mu = numpy.array([float(start[p]) for p in range(P)])
-    s2 = numpy.array([numpy.sqrt(numpy.abs(start[p]) / 10.) for p in range(P)])
-    sd = numpy.sqrt(s2)
+        group_ll = _host_batch_group_ll(family, sizes, off)
+    rss = [numpy.random.RandomState(c) for c in chains]
 
-    def draw(p):
-        # scipy norm(mu, sd).rvs(): standard_normal * scale + loc; no draw if scale == 0
-        if sd[p] == 0:
-            return mu[p]
-        return rs.standard_normal() * sd[p] + mu[p]
+    # ---- start points (:1066-1089), every chain in lock step --------------------
+    theta = numpy.zeros((C, P, G))
+    x = [None] * C
+    tries = [0] * C
+    pending = list(range(C))
+    for k in pending:
+        x[k] = _draw_start(names, rss[k], priors, ranges)
+    while pending:
+        for k in pending:
+            theta[k] = numpy.asarray(x[k], dtype=numpy.float64)[:, None]
+        with numpy.errstate(over="ignore", invalid="ignore"):
+            pooled = numpy.sum(group_ll(theta), axis=1)       # -objective(x), :1102-1105
+        again = []
+        for k in pending:
+            tries[k] += 1
+            if tries[k] > 1000:
+                raise RuntimeError("Failed to find a valid starting state: ll =", -pooled[k])
+            if not numpy.isfinite(pooled[k]):
+                x[k] = _draw_start(names, rss[k], priors, ranges)
+                again.append(k)
+        pending = again
+    if mle:   # :1107-1141 with the exact numpy objective, chains in parallel
+        def opt(k):
+            return _optimize_start(family, n_total, names, rss[k], priors, ranges, list(x[k]))
+        if threads > 1 and C > 1:
+            with ThreadPoolExecutor(max_workers=threads) as ex:
+                x = list(ex.map(opt, range(C)))
+        else:
+            x = [opt(k) for k in range(C)]
+    start = numpy.array([[float(v) for v in x[k]] for k in range(C)])   # [C, P]
 
-    value = numpy.empty((P, G))
-    lp = numpy.empty((P, G))
-    for p in range(P):
-        for g in range(G):
-            value[p, g] = draw(p)
-            lp[p, g] = _norm_logpdf(value[p, g], mu[p], sd[p])
-    LL = numpy.full(G, numpy.nan)
-    ll = numpy.full(G, -numpy.inf)
-    while not numpy.all(numpy.isfinite(ll)):
-        ll = group_ll(value)
+    if pooling in ("none", "complete"):   # StepMethod._setStartingPoint (:584-592)
+        value = numpy.repeat(start[:, :, None], G, axis=2)
+        lp = numpy.empty((C, P, G))
         for p in range(P):
-            for g in range(G):
-                if numpy.isfinite(ll[g]):
-                    LL[g] = ll[g]
-                else:
-                    value[p, g] = draw(p)       # logPrior left stale (:284-285)
-    return ChainInit(value, lp, LL, mu, s2)
+            lp[:, p, :] = numpy.asarray(priors[p].logpdf(start[:, p]), dtype=numpy.float64)[:, None]
+        return dict(value=value, log_prior=lp, ll=numpy.full((C, G), numpy.nan), mu=None,
+                    s2=None)
+
+    # ---- partial (:725-758) ----------------------------------------------------
+    mu = start.copy()
+    s2 = numpy.sqrt(numpy.abs(start) / 10.)
+    sd = numpy.sqrt(s2)
+    value = numpy.empty((C, P, G))
+    lp = numpy.empty((C, P, G))
+    for k in range(C):
+        rs = rss[k]
+        for p in range(P):
+            # scipy norm(mu, sd).rvs(): standard_normal * scale + loc; no draw if scale == 0
+            if sd[k, p] == 0:
+                value[k, p] = mu[k, p]
+            else:
+                value[k, p] = rs.standard_normal(G) * sd[k, p] + mu[k, p]
+            lp[k, p] = _norm_logpdf_groups(value[k, p], mu[k, p], sd[k, p])
+    LL = numpy.full((C, G), numpy.nan)
+    pending = list(range(C))
+    while pending:
+        ll = group_ll(value)
+        again = []
+        for k in pending:
+            fin = numpy.isfinite(ll[k])
+            LL[k, fin] = ll[k, fin]
+            if not fin.all():
+                rs = rss[k]
+                for p in range(P):        # _determineIndividualStartingPoint order
+                    for g in numpy.flatnonzero(~fin):
+                        # samplePriorAndSetValue: logPrior left stale (:284-285)
+                        value[k, p, g] = (mu[k, p] if sd[k, p] == 0
+                                          else rs.standard_normal() * sd[k, p] + mu[k, p])
+                again.append(k)
+        pending = again
+    return dict(value=value, log_prior=lp, ll=LL, mu=mu, s2=s2)
 
 
-def init_chains(family, sizes, names, chains, pooling, priors, ranges, mle, threads=1):
-    """Stacked initial states for global chain ids ``chains``: dict of [C, ...] arrays."""
-    chains = list(chains)
+def _optimize_start(family, n_total, names, rs, priors, ranges, start):
+    """MCMC._optimizeStartingPoint (:1107-1141) from a found start point."""
+    def objective(xx):
+        return -1 * numpy.sum(family([numpy.full(n_total, float(v)) for v in xx]))
 
-    def one(c):
-        return init_chain(family, sizes, names, c, pooling, priors, ranges, mle)
-
-    if threads > 1 and len(chains) > 1:
-        with ThreadPoolExecutor(max_workers=threads) as ex:
-            inits = list(ex.map(one, chains))
-    else:
-        inits = [one(c) for c in chains]
-    out = dict(value=numpy.stack([i.value for i in inits]),
-               log_prior=numpy.stack([i.log_prior for i in inits]),
-               ll=numpy.stack([i.ll for i in inits]))
-    if pooling == "partial":
-        out["mu"] = numpy.stack([i.mu for i in inits])
-        out["s2"] = numpy.stack([i.s2 for i in inits])
-    else:
-        out["mu"] = out["s2"] = None
-    return out
+    n = 0
+    while True:
+        n += 1
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            res = scipy.optimize.minimize(objective, start, method="Nelder-Mead",
+                                          options={"maxiter": None, "maxfev": None,
+                                                   "xtol": 0.0001, "ftol": 0.0001})
+        if numpy.isfinite(res.fun):
+            start = res.x
+            if res.success:
+                break
+        else:
+            # the reference calls _findStartingPoint() without arguments here
+            # (:1131, a TypeError); restart the search instead.
+            start = find_starting_point(family, n_total, names, rs, priors, ranges, False)
+        if n > 10:
+            start = res.x
+            break
+    return start

@@ -4,8 +4,9 @@ Control flow of posteriorSampling.samplePosterior (:28-216) with the per-chain
 Python hot loop (MCMC/Sampler/StepMethod, :790-1158) replaced by libnestmc:
 
   validate + prepare directories/logs        (:147-168, :1018-1043)
-  host init of every chain, RandomState(c)   (:1060-1141, :725-758)   nestmc.init
   shard chains over GPUs (contiguous blocks of global chain ids)      nestmc.parallel
+  init of every chain, RandomState(c), LLs batched on its GPU
+                                             (:1060-1141, :725-758)   nestmc.init
   device loop: nmc_run over all iterations   (:862-896)               nestmc.engine
   device sample store -> sample.<c>.csv      (:898-936)               nestmc.output
   optional per-observation LL rows           (:890-891, :907-909)
@@ -126,7 +127,7 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
     devices = [0] if devices is None else list(devices)
     partial = pooling == "partial"
 
-    # ---- host initialisation (reference RNG order, RandomState(chain)) -----
+    # ---- chain logs; initialisation (reference RNG order, RandomState(chain)) ----
     if displayProgress:
         output.print_progress("Initialising %d chains." % len(chain_ids))
     chain_logs = []
@@ -136,10 +137,8 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
                                    loggingLevel)
             lg.info("chain %i. Started looking for a reasonable starting state." % c)
             chain_logs.append(lg)
-    st = init_chains(logLikelihoodFunction, sizes, names, chain_ids, pooling, start_priors,
-                     startingPointValueRange, startWithMLE, threads=threads)
-
-    # ---- shard contiguous blocks of chains over the devices -----------------
+    # ---- shard contiguous blocks of chains over the devices; every device
+    #      initialises its own chains, their likelihoods evaluated in batches on it --
     engines = []
     for r, dev in enumerate(devices):
         s0, cnt = shard(len(chain_ids), len(devices), r)
@@ -151,9 +150,10 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
         eng = Engine(logLikelihoodFunction, sizes, cnt, pooling, priors, seed=seed,
                      chain_base=ids[0], device=dev, rng=rng)
         sl = slice(s0, s0 + cnt)
-        eng.set_state(st["value"][sl], st["log_prior"][sl], st["ll"][sl],
-                      None if st["mu"] is None else st["mu"][sl],
-                      None if st["s2"] is None else st["s2"][sl])
+        st = init_chains(logLikelihoodFunction, sizes, names, ids, pooling, start_priors,
+                         startingPointValueRange, startWithMLE, threads=threads,
+                         group_ll=eng.eval_group_ll)
+        eng.set_state(st["value"], st["log_prior"], st["ll"], st["mu"], st["s2"])
         if replay is not None:
             eng.set_replay(*(numpy.asarray(replay[k])[sl] for k in ("z", "u", "hz", "hu")))
         eng.set_schedule(nIter, burn, thin, 100)

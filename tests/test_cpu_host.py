@@ -93,3 +93,28 @@ def test_prior_encoding():
     assert prm[:2] == [100.0, 10.0] and prm[4] == numpy.log(10.0)
     with pytest.raises(ValueError):
         priors.encode(scipy.stats.beta(2, 3))
+
+
+@pytest.mark.parametrize("name", ["regression_complete", "regression_none", "regression3_partial",
+                                  "linreg_partial", "linreg_ragged_partial", "distribution_none",
+                                  "distribution_partial", "logistic_partial"])
+def test_batched_init_matches_reference_order(name):
+    """nestmc.init.init_chains advances every chain's RandomState in lock step (one
+    batched likelihood call per round); the start points, MLE starts, values, log
+    priors (stale ones included, :284-285) and hyper starts must equal the oracle's
+    one-chain-at-a-time restatement of :1060-1141 / :725-758 exactly."""
+    from gpu_cases import family_for
+    from nestmc.init import init_chains
+    from oracle import restatement as rs
+    c = Case(name)
+    st = init_chains(family_for(c), c.sizes, c.names, range(c.n_chains), c.pooling, c.priors,
+                     c.ranges, c.mle)
+    nested = rs.Nested(c.ll, c.sizes)
+    for ch in range(c.n_chains):
+        o, _ = rs.init_chain(nested, c.names, ch, c.pooling, c.priors, c.ranges, c.mle)
+        assert numpy.array_equal(st["value"][ch], o.value[0])
+        assert numpy.array_equal(st["log_prior"][ch], o.lp[0], equal_nan=True)
+        assert numpy.allclose(st["ll"][ch], o.ll[0], equal_nan=True, rtol=1e-12, atol=0)
+        if c.pooling == "partial":
+            assert numpy.array_equal(st["mu"][ch], o.mu[0])
+            assert numpy.array_equal(st["s2"][ch], o.s2[0])
