@@ -131,9 +131,13 @@ int nmc_get_kernel_timing(nmc_ctx* ctx, double* step_ms_total, int64_t* step_lau
 /* Cap the iterations one persistent launch covers (0 = the variate chunk, the
  * default); e.g. equal-length launches for profiling.                           */
 int nmc_set_launch_iters(nmc_ctx* ctx, int max_iters);
-/* Launch geometry: waves per workgroup, 64-chain blocks, and whether one resident
- * launch runs a whole chunk of iterations (1) or one launch per iteration (0).   */
-int nmc_launch_config(nmc_ctx* ctx, int* waves_per_group, int* chain_blocks, int* persistent);
+/* Launch geometry of the step kernel: waves per workgroup, chain blocks, whether one
+ * resident launch runs a whole chunk of iterations (1) or one launch per iteration
+ * (0), chains per workgroup (64, or 32 in the half-lane layout) and the kernel mode
+ * (0 none/complete, 1 launch per iteration, 2 persistent sync, 3 LDS Gibbs payload,
+ * 4 register Gibbs hand-off, 5 pair); chains_per_block and mode may be NULL.      */
+int nmc_launch_config(nmc_ctx* ctx, int* waves_per_group, int* chain_blocks, int* persistent,
+                      int* chains_per_block, int* mode);
 
 /* Sampler._printSample (:902-905) + _print (:933-936): append rows of local
  * chain c to a CSV file with the reference's "%i,%i,%f,..." formatting (and the

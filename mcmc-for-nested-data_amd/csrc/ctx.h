@@ -8,6 +8,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <string>
 #include <utility>
 #include <vector>

@@ -46,6 +46,12 @@
 
 struct Dev {
   int C, G, P, pooling, nf, chain_base, rng_mode, W, CB;
+  // step kernel: chains per workgroup (64: one chain per lane; 32: the half-lane layout,
+  // lanes l and l + 32 hold the same chain and split every row pair of the likelihood,
+  // so two workgroups share a CU where one 64-chain workgroup would hold it alone) and
+  // its chain blocks RB = ceil(C / CL).  CB = ceil(C / 64) for every other kernel.
+  int CL, RB;
+  int paired;            // likelihood rows: two chains per lane (nmc_ll_rows_lds<Fam, true>)
   uint32_t seed;
   const int64_t* off;    // [G+1] CSR offsets
   const double* obs;     // [n_obs][nf]
@@ -142,6 +148,28 @@ struct Dev {
 #define NMC_STAMP(t, slot) do {} while (0)
 #define NMC_STAMP_AT(k, slot) do {} while (0)
 #endif
+
+// The chain of this lane in step-kernel chain block cb, and whether the lane owns its
+// outputs (half-lane layout: lanes 32-63 mirror lanes 0-31 and store nothing).
+__device__ __forceinline__ int nmc_lane_chain(const Dev& d, int cb, int lane) {
+  return cb * d.CL + (lane & (d.CL - 1));
+}
+__device__ __forceinline__ bool nmc_lane_owns(const Dev& d, int c, int lane) {
+  return c < d.C && lane < d.CL;
+}
+
+// Both halves' values of v in every lane (v_permlane32_swap, gfx950): lo = lanes 0-31's
+// value of the lane's pair, hi = lanes 32-63's.
+struct nmc_pair2 { double lo, hi; };
+__device__ __forceinline__ nmc_pair2 nmc_halves(double v) {
+  const unsigned l = (unsigned)__double2loint(v), h = (unsigned)__double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(l, l, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(h, h, false, false);
+  nmc_pair2 r;
+  r.lo = __hiloint2double((int)b[0], (int)a[0]);
+  r.hi = __hiloint2double((int)b[1], (int)a[1]);
+  return r;
+}
 
 enum { NMC_RUN_HYPER_LOAD = 1 };
 // Likelihood tiles per group (nmc_tiles) = partial-sum slots per accumulator.
@@ -348,7 +376,7 @@ __device__ __forceinline__ void nmc_hyper_variates(const Dev& d, int cb, int t, 
                                                    const nmc_lds_layout& L, int w0, int nw) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c = cb * 64 + lane;
+  const int c = nmc_lane_chain(d, cb, lane);
   const int cc = c < d.C ? c : d.C - 1;
   for (int p = w - w0; p >= 0 && p < d.P; p += nw)
     nmc_dma16(d.vh + (((size_t)(t - d.vbase) * d.P + p) * d.C + cc) * 2,
@@ -362,8 +390,9 @@ __device__ __forceinline__ void nmc_hyper(const Dev& d, const double* src, int c
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int W = blockDim.x >> 6;
   const int P = d.P, G = d.G, C = d.C;
-  const int c = cb * 64 + lane;
+  const int c = nmc_lane_chain(d, cb, lane);
   const int cc = c < C ? c : C - 1;
+  const bool own = nmc_lane_owns(d, c, lane);
   nmc_hyper_streams<SRC, false>(d, src, cc, lds, L);
   __syncthreads();
   for (int p = w; p < P; p += W) {
@@ -390,7 +419,7 @@ __device__ __forceinline__ void nmc_hyper(const Dev& d, const double* src, int c
     lds[(L.hyp + NMC_HY_LSD * P + p) * 64 + lane] = lsd;
     lds[(L.hyp + NMC_HY_S2 * P + p) * 64 + lane] = s2n;
     lds[(L.hyp + NMC_HY_ISD * P + p) * 64 + lane] = 1.0 / sdn;
-    if (write && c < C) {
+    if (write && own) {
       const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
       d.mu[ho] = m;
       d.s2[ho] = s2n;
@@ -540,16 +569,98 @@ __device__ __forceinline__ void nmc_rows_lds_linreg2(const double* p, int nb, do
         "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255", "scc", "memory");
 }
 
+// The paired-chain form of the same loop (NMC_ROWS_PAIRED): lanes 0-31 read row 2m and
+// lanes 32-63 row 2m+1 of every row pair m, and each lane evaluates its row for TWO
+// chains -- its own and its partner lane's (lane ^ 32) -- so one ds_read_b128 feeds 128
+// (chain, row) terms instead of 64: half the LDS instructions for the same fp64 work.
+// An 8-row block is four reads (rows v[b:b+15], residual temporaries v[t:t+7]); row pair
+// m feeds the own chain's u0/u1 and the partner's w0/w1 (m even / odd).  In half h those
+// are the full loop's a[h] / a[2 + h] of the respective chain, with the same rows in the
+// same order, and nmc_ll_rows_lds<Fam, true> reassembles them (one lane swap), so the
+// sums are bit-identical to the broadcast loop.  p: this half's first row (tile start +
+// h rows); nb: even number of 8-row blocks >= 2.
+#define NMC_P4(b, off)                                                     \
+  "ds_read_b128 v[" #b "+0:" #b "+3], %[addr] offset:" #off "+0\n"         \
+  "ds_read_b128 v[" #b "+4:" #b "+7], %[addr] offset:" #off "+32\n"        \
+  "ds_read_b128 v[" #b "+8:" #b "+11], %[addr] offset:" #off "+64\n"       \
+  "ds_read_b128 v[" #b "+12:" #b "+15], %[addr] offset:" #off "+96\n"
+// partner residual seed c0 - y into t, own b0 - y in place of y, then both fmas with x
+#define NMC_PDX(b, t, k4, k2) \
+  "v_add_f64 v[" #t "+" #k2 ":" #t "+" #k2 "+1], %[c0], -v[" #b "+" #k4 "+2:" #b "+" #k4 "+3]\n"
+#define NMC_PDO(b, k4) \
+  "v_add_f64 v[" #b "+" #k4 "+2:" #b "+" #k4 "+3], %[b0], -v[" #b "+" #k4 "+2:" #b "+" #k4 "+3]\n"
+#define NMC_PEO(b, k4)                                                                      \
+  "v_fma_f64 v[" #b "+" #k4 "+2:" #b "+" #k4 "+3], v[" #b "+" #k4 ":" #b "+" #k4 "+1], %[b1], v[" \
+  #b "+" #k4 "+2:" #b "+" #k4 "+3]\n"
+#define NMC_PEX(b, t, k4, k2)                                                               \
+  "v_fma_f64 v[" #t "+" #k2 ":" #t "+" #k2 "+1], v[" #b "+" #k4 ":" #b "+" #k4 "+1], %[c1], v[" \
+  #t "+" #k2 ":" #t "+" #k2 "+1]\n"
+#define NMC_PSO(b, k4, a) \
+  "v_fma_f64 %[" #a "], v[" #b "+" #k4 "+2:" #b "+" #k4 "+3], v[" #b "+" #k4 "+2:" #b "+" #k4 "+3], %[" #a "]\n"
+#define NMC_PSX(t, k2, a) \
+  "v_fma_f64 %[" #a "], v[" #t "+" #k2 ":" #t "+" #k2 "+1], v[" #t "+" #k2 ":" #t "+" #k2 "+1], %[" #a "]\n"
+#define NMC_PB(b, t)                                                                        \
+  NMC_PDX(b, t, 0, 0) NMC_PDX(b, t, 4, 2) NMC_PDX(b, t, 8, 4) NMC_PDX(b, t, 12, 6)           \
+  NMC_PDO(b, 0) NMC_PDO(b, 4) NMC_PDO(b, 8) NMC_PDO(b, 12)                                   \
+  NMC_PEO(b, 0) NMC_PEO(b, 4) NMC_PEO(b, 8) NMC_PEO(b, 12)                                   \
+  NMC_PEX(b, t, 0, 0) NMC_PEX(b, t, 4, 2) NMC_PEX(b, t, 8, 4) NMC_PEX(b, t, 12, 6)           \
+  NMC_PSO(b, 0, u0) NMC_PSO(b, 4, u1) NMC_PSO(b, 8, u0) NMC_PSO(b, 12, u1)                   \
+  NMC_PSX(t, 0, w0) NMC_PSX(t, 2, w1) NMC_PSX(t, 4, w0) NMC_PSX(t, 6, w1)
+__device__ __forceinline__ void nmc_rows_lds_linreg2_paired(const double* p, int nb, double b0,
+                                                            double b1, double c0, double c1,
+                                                            double& u0, double& u1, double& w0,
+                                                            double& w1) {
+  unsigned addr = (unsigned)(uintptr_t)(nmc_lds_cptr)p;
+  int cnt = nb;
+  asm volatile(
+      NMC_P4(208, 0)
+      "L_nmc_prows_%=:\n"
+      NMC_P4(232, 128)
+      "s_waitcnt lgkmcnt(4)\n"
+      NMC_PB(208, 224)
+      "v_add_u32 %[addr], 0x100, %[addr]\n"
+      "s_sub_u32 %[cnt], %[cnt], 2\n"
+      "s_cmp_gt_i32 %[cnt], 0\n"
+      "s_cbranch_scc0 L_nmc_plast_%=\n"
+      NMC_P4(208, 0)
+      "s_waitcnt lgkmcnt(4)\n"
+      NMC_PB(232, 248)
+      "s_branch L_nmc_prows_%=\n"
+      "L_nmc_plast_%=:\n"
+      "s_waitcnt lgkmcnt(0)\n"
+      NMC_PB(232, 248)
+      : [addr] "+v"(addr), [cnt] "+s"(cnt), [u0] "+v"(u0), [u1] "+v"(u1), [w0] "+v"(w0),
+        [w1] "+v"(w1)
+      : [b0] "v"(b0), [b1] "v"(b1), [c0] "v"(c0), [c1] "v"(c1)
+      : "v208", "v209", "v210", "v211", "v212", "v213", "v214", "v215", "v216", "v217", "v218",
+        "v219", "v220", "v221", "v222", "v223", "v224", "v225", "v226", "v227", "v228", "v229",
+        "v230", "v231", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240",
+        "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251",
+        "v252", "v253", "v254", "v255", "scc", "memory");
+}
+
 // The same over rows staged in LDS: blocks of R rows read with wave-uniform
 // (broadcast) ds_reads; block b+1 is requested before block b is consumed (LDS
 // returns in order, so the wait covers only block b).
 #ifndef NMC_LDS_ROW_DOUBLES
 #define NMC_LDS_ROW_DOUBLES 16   // doubles per software-pipelined LDS block (8 regression rows)
 #endif
+// PAIRED (NMC_ROWS_PAIRED): the R-row blocks are split by row parity between the two
+// lane halves and every lane evaluates its rows for its own chain (reg) and its partner
+// lane's (preg); one lane swap hands each chain the other parity's accumulators, then
+// the tail rows are added in order per chain -- bit-identical to PAIRED == false.
 template <class Fam>
+constexpr bool nmc_paired_rows_ok() {
+  constexpr int NF = Fam::NFIELDS;
+  constexpr int BD = NF <= 2 ? 16 : 8;
+  constexpr int R = (BD / NF) > 0 ? (BD / NF) : 1;
+  return R % 2 == 0;
+}
+template <class Fam, bool PAIRED = false>
 __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename Fam::Reg& reg,
                                                 const double* __restrict__ p, int n,
-                                                double (&acc)[Fam::NACC]) {
+                                                double (&acc)[Fam::NACC],
+                                                const typename Fam::Reg* preg = nullptr) {
   constexpr int NF = Fam::NFIELDS;
   // 8-row blocks for 2-field rows (measured: -17 % per iteration for regression),
   // 8 doubles otherwise (register pressure of the wider families)
@@ -567,7 +678,65 @@ __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename F
   // copies): the last prefetch reads one block past the range, which the LDS row
   // area is padded for (nmc_lds) and which is never consumed.
   const int nb2 = (n / R) & ~1;
-  if constexpr (Fam::ASM_ROWS) {
+  if constexpr (PAIRED) {
+    static_assert(R % 2 == 0, "the paired split needs row pairs in every block");
+    constexpr int RH = R / 2;
+    const int h = (threadIdx.x >> 5) & 1;
+    const double* ph = p + (size_t)h * NF;   // row 2m + h of pair m
+    double u[2][Fam::NACC], v[2][Fam::NACC];   // own chain / partner chain, m even / odd
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int k = 0; k < Fam::NACC; ++k) u[s][k] = v[s][k] = 0.0;
+    if constexpr (Fam::ASM_ROWS) {
+      static_assert(R == 8 && NF == 2, "the asm row loop is the 8-row {x, y} block");
+      if (nb2 > 0)
+        nmc_rows_lds_linreg2_paired(ph, nb2, reg.b0, reg.b[0], preg->b0, preg->b[0], u[0][0],
+                                    u[1][0], v[0][0], v[1][0]);
+    } else if (nb2 > 0) {
+      double A[RH * NF], B[RH * NF];
+#pragma unroll
+      for (int m = 0; m < RH; ++m)
+#pragma unroll
+        for (int f = 0; f < NF; ++f) A[m * NF + f] = ph[(size_t)2 * m * NF + f];
+      for (int b = 0; b < nb2; b += 2) {
+        const double* q = ph + (size_t)b * (R * NF);
+#pragma unroll
+        for (int m = 0; m < RH; ++m)
+#pragma unroll
+          for (int f = 0; f < NF; ++f) B[m * NF + f] = q[R * NF + (size_t)2 * m * NF + f];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < RH; ++m) {
+          fam.accum(reg, A + m * NF, u[m & 1]);
+          fam.accum(*preg, A + m * NF, v[m & 1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < RH; ++m)
+#pragma unroll
+          for (int f = 0; f < NF; ++f) A[m * NF + f] = q[2 * R * NF + (size_t)2 * m * NF + f];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < RH; ++m) {
+          fam.accum(reg, B + m * NF, u[m & 1]);
+          fam.accum(*preg, B + m * NF, v[m & 1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // own chain: a[2k + h] = u[k]; a[2k + 1 - h] = the partner lane's v[k] (the partner's
+    // partner chain is this lane's chain)
+#pragma unroll
+    for (int k = 0; k < Fam::NACC; ++k) {
+      const nmc_pair2 e = nmc_halves(v[0][k]), o = nmc_halves(v[1][k]);
+      const double p0 = h ? e.lo : e.hi, p1 = h ? o.lo : o.hi;
+      a[0][k] = h ? p0 : u[0][k];
+      a[1][k] = h ? u[0][k] : p0;
+      a[2][k] = h ? p1 : u[1][k];
+      a[3][k] = h ? u[1][k] : p1;
+    }
+  } else if constexpr (Fam::ASM_ROWS) {
     static_assert(R == 8 && NF == 2, "the asm row loop is the 8-row {x, y} block");
     if (nb2 > 0) nmc_rows_lds_linreg2(p, nb2, reg.b0, reg.b[0], a[0][0], a[1][0], a[2][0], a[3][0]);
   } else if (nb2 > 0) {
@@ -735,7 +904,7 @@ __device__ __forceinline__ void nmc_hyper_compute(const Dev& d, int cb, int t, i
                                                   double hx, int hoff) {
   const int lane = threadIdx.x & 63;
   const int P = d.P, G = d.G, C = d.C;
-  const int c = cb * 64 + lane;
+  const int c = nmc_lane_chain(d, cb, lane);
   const double* hv = lds + (size_t)(L.hval + hoff) * 64 + lane;   // hv[i * 64]: group i of p
   double* hy = lds + L.hyp * 64 + lane;
   const double sdm = sqrt(hy[(NMC_HY_S2 * P + p) * 64] / G);
@@ -795,7 +964,7 @@ __device__ __forceinline__ void nmc_hyper_compute(const Dev& d, int cb, int t, i
   hy[(NMC_HY_LSD * P + p) * 64] = lsd;
   hy[(NMC_HY_S2 * P + p) * 64] = s2n;
   hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
-  if (write && c < C) {
+  if (write && nmc_lane_owns(d, c, lane)) {
     const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
     d.mu[ho] = mu;
     d.s2[ho] = s2n;
@@ -868,7 +1037,7 @@ __device__ __forceinline__ void nmc_hyper_compute_reg(const Dev& d, int cb, int 
                                                       const double (&x)[64]) {
   const int lane = threadIdx.x & 63;
   const int P = d.P, G = d.G, C = d.C;
-  const int c = cb * 64 + lane;
+  const int c = nmc_lane_chain(d, cb, lane);
   double* hy = lds + hyp * 64 + lane;
   const double sdm = sqrt(hy[(NMC_HY_S2 * P + p) * 64] / G);
   const double tot = nmc_pairwise_reg(x, G, false, 0.0);
@@ -885,7 +1054,7 @@ __device__ __forceinline__ void nmc_hyper_compute_reg(const Dev& d, int cb, int 
   hy[(NMC_HY_LSD * P + p) * 64] = lsd;
   hy[(NMC_HY_S2 * P + p) * 64] = s2n;
   hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
-  if (write && c < C) {
+  if (write && nmc_lane_owns(d, c, lane)) {
     const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
     d.mu[ho] = mu;
     d.s2[ho] = s2n;
@@ -958,9 +1127,9 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const int P = d.P, G = d.G, C = d.C;
   const int b = blockIdx.x;
   const int g = b % G, cb = b / G;
-  const int c = cb * 64 + lane;
-  const bool live = c < C;
-  const int cc = live ? c : C - 1;
+  const int c = nmc_lane_chain(d, cb, lane);
+  const bool live = nmc_lane_owns(d, c, lane);
+  const int cc = c < C ? c : C - 1;
   constexpr bool sync =
       MODE == NMC_MODE_SYNC || MODE == NMC_MODE_SYNC_LDS || MODE == NMC_MODE_SYNC_REG;
   // Gibbs-wave modes: payload in LDS (two-stage pipeline) or in registers (one stage)
@@ -1071,9 +1240,68 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     }
     pend_p = -1;
   };
-  // ---- register mode: the Gibbs wave runs its own loop (no likelihood tiles), so its
-  //      64-value payload never shares registers with the control and tile code; it
-  //      meets the other waves at the same two barriers per step ----
+  // ---- the likelihood of step (t, p)'s proposal (:615-635), tile by tile: the wave
+  //      takes row tiles from the step's LDS counter until none is left; `between` runs
+  //      after its first tile (the control wave's pre-barrier work) ----
+  auto lik_tiles = [&](int t, int p, int sp, auto&& between) {
+    double thp[Fam::MAXP];
+#pragma unroll
+    for (int q = 0; q < Fam::MAXP; ++q) thp[q] = q < P ? th[q * 64] : 0.0;
+    const double prop = thp[p] + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
+                                     lds[(L.zl + 2 * sp) * 64 + 2 * lane];
+#pragma unroll
+    for (int q = 0; q < Fam::MAXP; ++q)
+      if (q == p) thp[q] = prop;
+    const typename Fam::Reg reg = fam.prepare(thp);
+    // paired rows: the partner lane's (lane ^ 32) proposal parameters
+    typename Fam::Reg preg = reg;
+    if constexpr (nmc_paired_rows_ok<Fam>()) if (d.paired) {
+      const bool hi = lane >= 32;
+#pragma unroll
+      for (int q = 0; q < Fam::MAXP; ++q) {
+        const nmc_pair2 e = nmc_halves(thp[q]);
+        thp[q] = hi ? e.lo : e.hi;
+      }
+      preg = fam.prepare(thp);
+    }
+    // the next tile is requested before the current one is computed: the atomic's
+    // return rides under the tile's own row reads
+    auto grab = [&]() -> unsigned {
+      unsigned k = 0;
+      if (lane == 0)
+        k = __hip_atomic_fetch_add(tcnt + sp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return k;
+    };
+    int k = (int)__builtin_amdgcn_readlane(grab(), 0);
+    (void)t;
+    while (k < nt) {
+      const unsigned kn = grab();
+      const int ra = TI.start(k);
+      const int rn = TI.len(k);
+      NMC_TILE_STAMP(k, 0);
+      double acc[Fam::NACC];
+      bool done = false;
+      if constexpr (nmc_paired_rows_ok<Fam>()) if (d.rows_lds && d.paired) {
+        // two chains per lane, row pairs split by lane half
+        nmc_ll_rows_lds<Fam, true>(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc, &preg);
+        done = true;
+      }
+      if (done) {
+      } else if (d.rows_lds) {   // wave-uniform LDS address: broadcast ds_reads, pipelined
+        nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
+      } else {          // wave-uniform global address: scalar loads
+        nmc_ll_rows(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, acc);
+      }
+#pragma unroll
+      for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = acc[j];
+      NMC_TILE_STAMP(k, 1);
+      between();
+      k = (int)__builtin_amdgcn_readlane(kn, 0);
+    }
+  };
+  // ---- register mode: the Gibbs wave runs its own loop, so its 64-value payload never
+  //      shares registers with the control code; after its update it takes likelihood
+  //      tiles like every other wave, and it meets them at the same two barriers ----
   if constexpr (hr) if (gw) {
     const int gs0 = i0 * P;
     for (int t = i0; t < i1 && ok; ++t) {
@@ -1111,6 +1339,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             }
           }
         }
+        lik_tiles(t, p, gs & 1, []() {});
         __syncthreads();   // A
         if (due) {
           ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
@@ -1178,7 +1407,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             // keep the payload loads below the poll (no instruction: wavefront scope)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const double* src = (atq & 1) ? d.vb1 : d.vb0;
-            if ((C & 1) == 0) {
+            if ((C & 1) == 0 && d.CL == 64) {
               nmc_hyper_dma(d, src, aq, cb, 0, G, lds, L, 0);
               nmc_drain_vm();
             } else {
@@ -1232,7 +1461,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             // keep the payload loads below the poll (no instruction: wavefront scope)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const double* src = (atq & 1) ? d.vb1 : d.vb0;
-            if ((C & 1) == 0)
+            if ((C & 1) == 0 && d.CL == 64)
               nmc_hyper_dma(d, src, aq, cb, 0, G, lds, L, ((gs - 1) & 1) * (G + 1));
             else
               nmc_hyper_load(d, src, aq, cc, 0, G, lds, L, ((gs - 1) & 1) * (G + 1));
@@ -1291,48 +1520,15 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         ctl_done = true;
       }
       // ---- likelihood of the proposal (:615-635), tile by tile, every wave ----
-      {
-        double thp[Fam::MAXP];
-#pragma unroll
-        for (int q = 0; q < Fam::MAXP; ++q) thp[q] = q < P ? th[q * 64] : 0.0;
-        const double prop = thp[p] + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
-                                         lds[(L.zl + 2 * sp) * 64 + 2 * lane];
-#pragma unroll
-        for (int q = 0; q < Fam::MAXP; ++q)
-          if (q == p) thp[q] = prop;
-        const typename Fam::Reg reg = fam.prepare(thp);
-        // the next tile is requested before the current one is computed: the atomic's
-        // return rides under the tile's own row reads
-        auto grab = [&]() -> unsigned {
-          unsigned k = 0;
-          if (lane == 0)
-            k = __hip_atomic_fetch_add(tcnt + sp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          return k;
-        };
-        int k = (int)__builtin_amdgcn_readlane(grab(), 0);
-        while (k < nt) {
-          const unsigned kn = grab();
-          const int ra = TI.start(k);
-          const int rn = TI.len(k);
-          NMC_TILE_STAMP(k, 0);
-          double acc[Fam::NACC];
-          if (d.rows_lds)   // wave-uniform LDS address: broadcast ds_reads, software-pipelined
-            nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
-          else              // wave-uniform global address: scalar loads
-            nmc_ll_rows(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, acc);
-#pragma unroll
-          for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = acc[j];
-          NMC_TILE_STAMP(k, 1);
-          if (!ctl_done) {
-            ctl_work();
-            ctl_done = true;
-          }
-          k = (int)__builtin_amdgcn_readlane(kn, 0);
-        }
-        if (!ctl_done) {   // (no tile left for the control wave)
+      lik_tiles(t, p, sp, [&]() {
+        if (!ctl_done) {
           ctl_work();
           ctl_done = true;
         }
+      });
+      if (!ctl_done) {   // (no tile left for the control wave)
+        ctl_work();
+        ctl_done = true;
       }
       NMC_STAMP(t, 1 + 3 * (p & 1));
       if (ctl || (hl && !pipe && gw)) nmc_drain_vm();   // this wave's LDS-DMA has landed
@@ -1455,7 +1651,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     if (!hr && pub && gw) {
       const double* src = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
       const int ho = ((ge - 1) & 1) * (G + 1);
-      if ((C & 1) == 0) {
+      if ((C & 1) == 0 && d.CL == 64) {
         nmc_hyper_dma(d, src, P - 1, cb, 0, G, lds, L, ho);
         nmc_drain_vm();
       } else {

@@ -57,14 +57,14 @@ __global__ void __launch_bounds__(256) nmc_k_fill(Dev d, int iter0, int T) {
 }
 
 // Gibbs update after iteration t alone (closes a chunk in launch-per-iteration mode);
-// grid = CB workgroups.
+// grid = RB workgroups (the step kernel's chain blocks).
 __global__ void __launch_bounds__(1024) nmc_k_hyper(Dev d, const double* src, int t) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int W = blockDim.x >> 6;
   const int P = d.P, C = d.C;
-  const int c = blockIdx.x * 64 + lane;
+  const int c = nmc_lane_chain(d, blockIdx.x, lane);
   const int cc = c < C ? c : C - 1;
   const nmc_lds_layout L = nmc_lds(0, P, 1, d.nleaf, d.ntail, 0, d.G, 0);
   for (int p = w; p < P; p += W) {

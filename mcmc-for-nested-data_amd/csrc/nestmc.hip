@@ -61,10 +61,12 @@ static void choose_geometry(nmc_ctx* x) {
   if (x->pooling == NMC_POOL_PARTIAL && w >= 2) w += 1;
   if (w > 8) w = 8;
   if (w < 1) w = 1;
+  d.CL = 64;   // one chain per lane, every kernel
   if (const char* e = getenv("NMC_WAVES")) {
     const int v = atoi(e);
     if (v >= 1 && v <= 8) w = v;
   }
+  d.RB = (d.C + d.CL - 1) / d.CL;
   d.W = (int)w;
   d.tile = 64;   // rows per likelihood tile (a multiple of 16); diagnostics override below
   if (const char* e = getenv("NMC_TILE_ROWS")) {
@@ -77,6 +79,7 @@ static void choose_geometry(nmc_ctx* x) {
   d.rows_lds = (size_t)d.nmax * x->nf * 8 <= (size_t)64 * 1024 &&
                lds_bytes_for(x, 0, 1) <= (size_t)96 * 1024 &&
                !(getenv("NMC_NO_LDS_ROWS") && atoi(getenv("NMC_NO_LDS_ROWS")));
+
   // the persistent Gibbs update by the auxiliary waves needs G <= 128 (one numpy
   // leaf) and one parameter's chain-block values in LDS
   d.noprio = getenv("NMC_NOPRIO") ? atoi(getenv("NMC_NOPRIO")) : 0;   // diagnostics bits
@@ -94,6 +97,11 @@ static void choose_geometry(nmc_ctx* x) {
            (size_t)nmc_pair_lds(x->nacc, d.nmax * x->nf).total * 512 <= (size_t)160 * 1024 &&
            getenv("NMC_PAIR") && atoi(getenv("NMC_PAIR"));
   if (d.pair && d.W < 4) d.W = 4;
+  // likelihood rows in LDS for a family whose row blocks pair up (<= 4 fields): each lane
+  // evaluates its rows for two chains (kernels.h nmc_ll_rows_lds<Fam, true>), half the LDS
+  // reads; NMC_ROWS=bcast keeps the one-chain broadcast loop (same sums bit for bit)
+  d.paired = d.rows_lds && x->nf <= 4;
+  if (const char* e = getenv("NMC_ROWS")) d.paired = d.paired && strcmp(e, "bcast") != 0;
 }
 
 // numpy's pairwise-sum recursion over G groups (numpy/_core/src/umath/loops_utils.h):
@@ -121,7 +129,7 @@ static int launch_hyper(nmc_ctx* x, int t) {
   }
   const Dev& d = x->d;
   const size_t lds = (size_t)nmc_lds(0, d.P, 1, d.nleaf, d.ntail, 0, d.G, 0).total * 512;
-  hipLaunchKernelGGL(nmc_k_hyper, dim3(d.CB), dim3(64 * d.W), lds, x->stream, x->d,
+  hipLaunchKernelGGL(nmc_k_hyper, dim3(d.RB), dim3(64 * d.W), lds, x->stream, x->d,
                      (const double*)vslot(x, t & 1), t);
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev->second, x->stream));
@@ -249,7 +257,8 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   int* dmerge = nullptr;
   rc |= dalloc(x, &dleaf, starts.size());
   rc |= dalloc(x, &dmerge, merges.size());
-  rc |= dalloc(x, &d.cnt, (size_t)32 * 8 * d.CB * n_params);   // [CB][P][8 shards][32]
+  // [RB][P][8 shards][32], RB <= ceil(C / 32)
+  rc |= dalloc(x, &d.cnt, (size_t)32 * 8 * ((n_chains + 31) / 32) * n_params);
   rc |= dalloc(x, &d.tmo, 4);
   if (rc) { nmc_destroy(x); return rc; }
   d.leaf = dleaf;
@@ -481,7 +490,7 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       if (!partial) {
         if (int rc = launch_run(c0, c1, 0)) return rc;
       } else if (x->persistent) {
-        HIPCHK(hipMemsetAsync(x->d.cnt, 0, (size_t)32 * 8 * x->d.CB * x->P * sizeof(unsigned),
+        HIPCHK(hipMemsetAsync(x->d.cnt, 0, (size_t)32 * 8 * x->d.RB * x->P * sizeof(unsigned),
                               x->stream));
         if (int rc = launch_run(c0, c1, NMC_RUN_HYPER_LOAD)) return rc;
       } else {
@@ -621,10 +630,13 @@ int nmc_get_kernel_timing(nmc_ctx* x, double* step_ms, int64_t* step_n, int64_t*
   return 0;
 }
 
-int nmc_launch_config(nmc_ctx* x, int* waves_per_group, int* chain_blocks, int* persistent) {
+int nmc_launch_config(nmc_ctx* x, int* waves_per_group, int* chain_blocks, int* persistent,
+                      int* chains_per_block, int* mode) {
   *waves_per_group = x->d.W;
-  *chain_blocks = x->d.CB;
+  *chain_blocks = x->d.RB;
   if (persistent) *persistent = x->persistent || x->pooling != NMC_POOL_PARTIAL ? 1 : 0;
+  if (chains_per_block) *chains_per_block = x->d.CL;
+  if (mode) *mode = run_mode(x);
   return 0;
 }
 

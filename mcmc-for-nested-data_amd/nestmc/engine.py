@@ -14,6 +14,10 @@ from . import _lib
 from . import priors as _priors
 from ._lib import as_f64, check, dptr
 
+# step-kernel modes reported by nmc_launch_config (kernels.h NMC_MODE_*)
+MODE_NAMES = {0: "NMC_MODE_NOPOOL", 1: "NMC_MODE_LAUNCH", 2: "NMC_MODE_SYNC",
+              3: "NMC_MODE_SYNC_LDS", 4: "NMC_MODE_SYNC_REG", 5: "NMC_MODE_PAIR"}
+
 
 class Engine:
     def __init__(self, family, sizes, n_chains, pooling, priors=None, *, seed=0,
@@ -209,7 +213,8 @@ class Engine:
                     hyper_ms=hm.value, hyper_launches=hn.value)
 
     def launch_config(self):
-        w, cb, pe = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        w, cb, pe, cl, md = (ctypes.c_int() for _ in range(5))
         check(self.lib.nmc_launch_config(self.h, ctypes.byref(w), ctypes.byref(cb),
-                                         ctypes.byref(pe)))
-        return dict(waves_per_group=w.value, chain_blocks=cb.value, persistent=bool(pe.value))
+                                         ctypes.byref(pe), ctypes.byref(cl), ctypes.byref(md)))
+        return dict(waves_per_group=w.value, chain_blocks=cb.value, persistent=bool(pe.value),
+                    chains_per_block=cl.value, mode=MODE_NAMES.get(md.value, str(md.value)))

@@ -180,3 +180,28 @@ def test_eval_group_ll_matches_oracle(gpu_lib):
     want = numpy.array([nested.group_ll(theta[c]) for c in range(C)])
     assert numpy.allclose(got, want, rtol=1e-11)
     eng.close()
+
+
+@pytest.mark.parametrize("kind,C,G,N,ragged,n_iter", [
+    ("linreg_partial", 70, 9, 40, True, 40),        # asm row loop, ragged, odd chain count
+    ("logistic_partial", 66, 5, 30, False, 30),     # generic loop, 4 fields (R = 2)
+    ("regression3_none", 65, 4, 25, False, 40),     # asm loop, sigma sampled, no pooling
+    ("gauss_none", 64, 6, 20, True, 30),            # generic loop, 3 fields
+    ("linreg_partial", 64, 64, 256, False, 12),     # register Gibbs hand-off, G = 64
+    ("logistic_partial", 96, 24, 200, True, 10),    # tails in every group
+])
+def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
+    """The paired-chain row loop (each lane evaluates its row pair half for its own chain
+    and for lane ^ 32's, kernels.h nmc_ll_rows_lds<Fam, true>) reproduces the one-chain
+    broadcast loop bit for bit: flags, proposal LLs and recorded rows."""
+    from gpu_cases import run_engine
+    fam, sizes, priors, pooling, names = synthetic(kind, C, G, N, ragged=ragged)
+    P = fam.n_params
+    st, _ = _synthetic_state(fam, sizes, priors, pooling, C, P, len(sizes))
+    runs = {}
+    for rows in ("paired", "bcast"):
+        runs[rows] = run_engine(fam, sizes, st, numpy.arange(C), 5, n_iter, 777, pooling=pooling,
+                                priors=priors, env={"NMC_ROWS": rows}, tune_interval=7)
+    for k in range(3):
+        assert numpy.array_equal(runs["paired"][k], runs["bcast"][k], equal_nan=True), k
+    assert runs["paired"][0].mean() > 0.02

@@ -4,8 +4,8 @@
   the chains (chain_base = 0 / C/2, as two ranks would) reproduce the one-engine
   run bit for bit -- the multi-GPU correctness argument, on one device;
 * cfg 3 at full size (256 chains x 64 groups x 1000 obs, partial pooling): the
-  persistent launch (auxiliary-wave Gibbs hand-off) and the launch-per-iteration
-  fallback are bit-identical (the likelihood partition and every summation order
+  persistent launch (register Gibbs hand-off, paired-chain row loop), the one-chain
+  broadcast row loop and the launch-per-iteration fallback are bit-identical (the likelihood partition and every summation order
   are launch-mode independent), and the first chains match the numpy oracle on the
   same Philox stream (flags exact, values within 1e-9).
 """
@@ -83,8 +83,11 @@ def test_cfg3_full_size_launch_modes_and_oracle(gpu_lib):
     assert pers[3]["persistent"], pers[3]
     launch = _run(fam, sizes, st, sel, 0, n_iter, seed, env={"NMC_PERSIST": "0"})
     assert not launch[3]["persistent"]
-    for k in range(3):
-        assert numpy.array_equal(pers[k], launch[k], equal_nan=True), k
+    bcast = _run(fam, sizes, st, sel, 0, n_iter, seed, env={"NMC_ROWS": "bcast"})
+    assert bcast[3]["persistent"], bcast[3]
+    for other in (launch, bcast):
+        for k in range(3):
+            assert numpy.array_equal(pers[k], other[k], equal_nan=True), k
     acc = pers[0]
     assert 0.05 < acc.mean() < 0.95
 
