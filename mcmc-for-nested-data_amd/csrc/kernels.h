@@ -173,7 +173,10 @@ __device__ __forceinline__ nmc_pair2 nmc_halves(double v) {
 
 enum { NMC_RUN_HYPER_LOAD = 1 };
 // Likelihood tiles per group (nmc_tiles) = partial-sum slots per accumulator.
-enum { NMC_NSLOT = 16 };
+#ifndef NMC_NSLOT_N
+#define NMC_NSLOT_N 16
+#endif
+enum { NMC_NSLOT = NMC_NSLOT_N };
 enum { NMC_SPIN_LIMIT = 1 << 22 };
 
 // Offset of the hyper-parameter slot holding the state after iteration t ([2][P][C]:
@@ -604,8 +607,8 @@ __device__ __forceinline__ void nmc_rows_lds_linreg2(const double* p, int nb, do
   NMC_PDO(b, 0) NMC_PDO(b, 4) NMC_PDO(b, 8) NMC_PDO(b, 12)                                   \
   NMC_PEO(b, 0) NMC_PEO(b, 4) NMC_PEO(b, 8) NMC_PEO(b, 12)                                   \
   NMC_PEX(b, t, 0, 0) NMC_PEX(b, t, 4, 2) NMC_PEX(b, t, 8, 4) NMC_PEX(b, t, 12, 6)           \
-  NMC_PSO(b, 0, u0) NMC_PSO(b, 4, u1) NMC_PSO(b, 8, u0) NMC_PSO(b, 12, u1)                   \
-  NMC_PSX(t, 0, w0) NMC_PSX(t, 2, w1) NMC_PSX(t, 4, w0) NMC_PSX(t, 6, w1)
+  NMC_PSO(b, 0, u0) NMC_PSX(t, 0, w0) NMC_PSO(b, 4, u1) NMC_PSX(t, 2, w1)                   \
+  NMC_PSO(b, 8, u0) NMC_PSX(t, 4, w0) NMC_PSO(b, 12, u1) NMC_PSX(t, 6, w1)
 __device__ __forceinline__ void nmc_rows_lds_linreg2_paired(const double* p, int nb, double b0,
                                                             double b1, double c0, double c1,
                                                             double& u0, double& u1, double& w0,
