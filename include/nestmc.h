@@ -138,6 +138,10 @@ int nmc_set_launch_iters(nmc_ctx* ctx, int max_iters);
  * 4 register Gibbs hand-off, 5 pair); chains_per_block and mode may be NULL.      */
 int nmc_launch_config(nmc_ctx* ctx, int* waves_per_group, int* chain_blocks, int* persistent,
                       int* chains_per_block, int* mode);
+/* Row split of none/complete pooling (CompletePooling._setGroupIndex :667-671 puts every
+ * observation in ONE group): members = workgroups sharing each (chain block, group),
+ * exchanging partial sums every step (1: no split); chain blocks per resident launch. */
+int nmc_split_config(nmc_ctx* ctx, int* members, int* chain_blocks_per_launch);
 
 /* Sampler._printSample (:902-905) + _print (:933-936): append rows of local
  * chain c to a CSV file with the reference's "%i,%i,%f,..." formatting (and the

@@ -54,6 +54,8 @@ struct nmc_ctx {
   bool persistent = false;                // partial pooling: one resident launch per chunk
   int ncu = 256;
   int* gidx = nullptr;                    // [n_obs] group of each observation (obs-LL rows)
+  int64_t nmax_group = 0;                 // rows of the largest group
+  int split_batch = 0;                    // row split: chain blocks per (resident) launch
 };
 
 static inline double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->d.vb0; }
@@ -102,7 +104,8 @@ enum {
   NMC_OP_CAN_PERSIST = 1,  // result = 1 if the persistent grid is co-resident
   NMC_OP_GROUP_LL = 2,     // in = theta [P][G][C] (device), out = [G][C] (device)
   NMC_OP_OBS_LL = 3,       // in = values [P][G][C] (device), out = [C][n_obs] (device)
-  NMC_OP_OBS_LL_ROWS = 4   // sample rows [i0, i1) -> out = [C][i1 - i0][n_obs] (device)
+  NMC_OP_OBS_LL_ROWS = 4,  // sample rows [i0, i1) -> out = [C][i1 - i0][n_obs] (device)
+  NMC_OP_CAPACITY = 5      // result = resident step-kernel workgroups on the device
 };
 struct NmcCall {
   int op = 0;

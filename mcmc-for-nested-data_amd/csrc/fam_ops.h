@@ -15,9 +15,19 @@ static int nmc_launch_run(nmc_ctx* x, const Fam& fam, int i0, int i1, int flags)
     x->kev_iters[x->kev_used - 1] = i1 - i0;
     HIPCHK(hipEventRecord(ev->first, x->stream));
   }
-  const dim3 grid(d.RB * d.G), block(64 * d.W);
+  const dim3 grid(d.RB * d.G * d.S), block(64 * d.W);
   switch (run_mode(x)) {
     case NMC_MODE_NOPOOL:
+      if (d.S > 1) {   // row split: resident batches of chain blocks
+        for (int cb0 = 0; cb0 < d.RB; cb0 += x->split_batch) {
+          Dev db = d;
+          db.cb0 = cb0;
+          const int nb = std::min(x->split_batch, d.RB - cb0);
+          hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_NOPOOL>), dim3(nb * d.G * d.S), block, lds,
+                             x->stream, db, fam, d.obs, i0, i1, flags);
+        }
+        break;
+      }
       hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_NOPOOL>), grid, block, lds, x->stream, d, fam,
                          d.obs, i0, i1, flags);
       break;
@@ -78,6 +88,16 @@ static int nmc_fam_call(nmc_ctx* x, const Fam& fam, NmcCall& c) {
     case NMC_OP_CAN_PERSIST:
       c.result = nmc_can_persist<Fam>(x) ? 1 : 0;
       return 0;
+    case NMC_OP_CAPACITY: {   // resident none/complete step-kernel workgroups (safe count)
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, nmc_k_run<Fam, NMC_MODE_NOPOOL>,
+                                                       64 * x->d.W, run_lds_bytes(x)) != hipSuccess)
+        return nmc_fail(-2, "occupancy query failed");
+      const int W = x->d.W;
+      const int safe = W % 4 == 0 ? std::min(nb, 24 / W) : (nb > 1 ? nb - 1 : nb);
+      c.result = safe * x->ncu;
+      return 0;
+    }
     case NMC_OP_GROUP_LL: {
       const size_t lds = (size_t)x->d.W * 64 * Fam::NACC * sizeof(double);
       hipLaunchKernelGGL(nmc_k_group_ll<Fam>, dim3(x->d.CB * x->G), dim3(64 * x->d.W), lds,

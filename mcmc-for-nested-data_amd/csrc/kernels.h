@@ -52,6 +52,16 @@ struct Dev {
   // its chain blocks RB = ceil(C / CL).  CB = ceil(C / 64) for every other kernel.
   int CL, RB;
   int paired;            // likelihood rows: two chains per lane (nmc_ll_rows_lds<Fam, true>)
+  // Row split (none/complete pooling with large groups): S workgroups ("members") share
+  // one (chain block, group), member m owning the m-th contiguous chunk of the group's
+  // rows (nmc_chunk); each step they exchange their partial sums through xbuf
+  // ([2 step parity][RB][G][S][NACC][64], sc1 stores + the unit's counter xcnt[RB*G][32])
+  // and all make the same decision.  S depends on the rows, the group count and the CU
+  // count only, never on the chain count: results are shard- and batch-invariant.
+  // cb0: first chain block of this launch (chain blocks are launched in resident batches).
+  int S, cb0;
+  double* xbuf;
+  unsigned* xcnt;
   uint32_t seed;
   const int64_t* off;    // [G+1] CSR offsets
   const double* obs;     // [n_obs][nf]
@@ -1088,6 +1098,62 @@ __device__ __forceinline__ void nmc_hyper_fetch_reg(const Dev& d, int tq, int q,
   hx = d.vh[hvi + 1];
 }
 
+// Row split: member m's partial sums of step k -> xbuf (sc1), counted on the unit's
+// counter; once all S members of step k have arrived, every member sums the S partials in
+// member order (four interleaved streams m & 3, combined (s0+s1)+(s2+s3)) -- identical in
+// every member.  A member is at most one step ahead of the slowest (it cannot pass step
+// k+1 before all partials of k+1 exist), so two step-parity slots suffice.  Call with
+// the whole (control) wave; bounded spin (d.tmo).
+template <int NA>
+__device__ __forceinline__ void nmc_split_exchange(const Dev& d, int cb, int g, int m, int k,
+                                                   double (&acc)[NA]) {
+  const int lane = threadIdx.x & 63;
+  const int S = d.S;
+  const size_t unit = (size_t)cb * d.G + g;
+  double* xb = d.xbuf + (((size_t)(k & 1) * d.RB * d.G + unit) * S) * NA * 64 + lane;
+#pragma unroll
+  for (int j = 0; j < NA; ++j)
+    __hip_atomic_store(xb + ((size_t)m * NA + j) * 64, acc[j], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  nmc_drain_vm();
+  unsigned* ctr = d.xcnt + unit * 32;
+  if (lane == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned target = (unsigned)S * (unsigned)(k + 1);
+  for (unsigned spins = 0;; ++spins) {
+    const unsigned v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v >= target) break;
+    if ((spins & 255) == 255 &&
+        __hip_atomic_load(d.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+      break;
+    if (spins >= NMC_SPIN_LIMIT) {
+      __hip_atomic_store(d.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  // keep the partial loads below the poll (no instruction: wavefront scope)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    double s4[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int m0 = 0; m0 < S; m0 += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = m0 + u < S ? __hip_atomic_load(xb + ((size_t)(m0 + u) * NA + j) * 64,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int mm = m0 + u;
+        if (mm < S) s4[mm & 3] = mm < 4 ? v[u] : s4[mm & 3] + v[u];
+      }
+    }
+    acc[j] = S >= 4 ? (s4[0] + s4[1]) + (s4[2] + s4[3])
+                    : (S == 1 ? s4[0] : (S == 2 ? s4[0] + s4[1] : (s4[0] + s4[1]) + s4[2]));
+  }
+}
+
 // ---------------------------------------------------------------------------
 // K_run: iterations [i0, i1) for every (chain, group); grid = CB*G workgroups of
 // 64*W threads (W <= 8); dynamic LDS = nmc_lds(...).total columns.
@@ -1129,9 +1195,11 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const int W = blockDim.x >> 6;
   const int P = d.P, G = d.G, C = d.C;
   const int b = blockIdx.x;
-  const int g = b % G, cb = b / G;
+  const int S = d.S;
+  const int mb = b % S;                           // row-split member (S == 1: 0)
+  const int g = (b / S) % G, cb = (b / S) / G + d.cb0;
   const int c = nmc_lane_chain(d, cb, lane);
-  const bool live = nmc_lane_owns(d, c, lane);
+  const bool live = nmc_lane_owns(d, c, lane) && mb == 0;   // member 0 writes the outputs
   const int cc = c < C ? c : C - 1;
   constexpr bool sync =
       MODE == NMC_MODE_SYNC || MODE == NMC_MODE_SYNC_LDS || MODE == NMC_MODE_SYNC_REG;
@@ -1151,8 +1219,10 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   double* hy = lds + L.hyp * 64 + lane;           // hy[(k * P + p) * 64]
   // tile counters, one per step parity (two 32-bit words in the flag column)
   unsigned* tcnt = (unsigned*)(lds + L.flag * 64 + 4);
-  const int64_t r0 = d.off[g];
-  const int nrow = (int)(d.off[g + 1] - r0);
+  const int ngrp = (int)(d.off[g + 1] - d.off[g]);   // the group's rows (finish)
+  int64_t r0;
+  int nrow;                                           // this member's rows
+  nmc_chunk(d.off[g], d.off[g + 1], mb, S, &r0, &nrow);
   const nmc_tiling TI = nmc_tiles(nrow, d.tile);
   const int nt = TI.nt;
   const double* grows = obs + r0 * Fam::NFIELDS;
@@ -1188,7 +1258,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / d.hsd[ho];
     }
   }
-  const double gcst = fam.gconst((long)nrow);   // per-group constant of finish_fast
+  const double gcst = fam.gconst((long)ngrp);   // per-group constant of finish_fast
   double* lrows = lds + L.rows * 64;
   if (d.rows_lds) {   // this group's rows -> LDS, once for the whole launch
     const int nd = nrow * Fam::NFIELDS;
@@ -1570,12 +1640,14 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         for (int j = 0; j < Fam::NACC; ++j) {
           acc[j] = nmc_sum_slots(lds + (L.part + j * NMC_NSLOT) * 64 + lane);
         }
+        if constexpr (!PARTIAL) if (S > 1)   // row split: every member's partials, in order
+          nmc_split_exchange(d, cb, g, mb, t * P + p - i0 * P, acc);
         if (p == 0) NMC_STAMP(t, 10);
         double thp[Fam::MAXP];
 #pragma unroll
         for (int q = 0; q < Fam::MAXP; ++q) thp[q] = q < P ? (q == p ? c_prop : th[q * 64]) : 0.0;
         const typename Fam::Reg reg = fam.prepare(thp);
-        const double llp = fam.finish_fast(reg, acc, (long)nrow, gcst);
+        const double llp = fam.finish_fast(reg, acc, (long)ngrp, gcst);
         if (p == 0) NMC_STAMP(t, 11);
         if (hl && post_prior) {   // the Gibbs wave evaluated this step's priors
           c_lpc = cwv[NMC_CW_LPC * 64];

@@ -270,7 +270,24 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   int64_t nmax = 0;
   for (int g = 0; g < n_groups; ++g)
     nmax = std::max<int64_t>(nmax, group_offsets[g + 1] - group_offsets[g]);
-  d.nmax = (int)nmax;
+  x->nmax_group = nmax;
+  // Row split (none/complete pooling): groups far larger than one workgroup's 64 KiB LDS
+  // row area are shared by S workgroups, at most 64 and at most one per CU per group.
+  // S depends on (rows, fields, groups, CU count) only -- never on the chain count -- so
+  // the partial-sum order, and every result, is the same whatever the sharding.
+  d.S = 1;
+  d.cb0 = 0;
+  if (pooling != NMC_POOL_PARTIAL) {
+    const int64_t target = std::max<int64_t>(256, (64 * 1024) / (n_fields * 8));
+    if (nmax > 2 * target)
+      d.S = (int)std::min<int64_t>({64, (nmax + target - 1) / target,
+                                    std::max<int64_t>(1, x->ncu / n_groups)});
+    if (const char* e = getenv("NMC_SPLIT")) {
+      const int v = atoi(e);
+      if (v >= 1 && v <= 64) d.S = v;
+    }
+  }
+  d.nmax = (int)((nmax + d.S - 1) / d.S);   // rows of the largest member
   choose_geometry(x);
   if (run_lds_bytes(x) > (size_t)160 * 1024) {
     nmc_destroy(x);
@@ -282,6 +299,24 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     c.op = NMC_OP_CAN_PERSIST;
     if (int rc2 = nmc_call_family(x, c)) { nmc_destroy(x); return rc2; }
     x->persistent = c.result == 1;
+  }
+  if (d.S > 1) {   // row split: resident batches of chain blocks, exchange buffers
+    NmcCall c;
+    c.op = NMC_OP_CAPACITY;
+    if (int rc2 = nmc_call_family(x, c)) { nmc_destroy(x); return rc2; }
+    const int64_t per_cb = (int64_t)d.G * d.S;
+    if (c.result < per_cb) {
+      nmc_destroy(x);
+      return fail(-1, "row split: the S workgroups of one group are not co-resident");
+    }
+    x->split_batch = (int)std::min<int64_t>(d.RB, c.result / per_cb);
+    if (const char* e = getenv("NMC_SPLIT_BATCH")) {
+      const int v = atoi(e);
+      if (v >= 1 && v < x->split_batch) x->split_batch = v;
+    }
+    rc |= dalloc(x, &d.xbuf, (size_t)2 * d.RB * d.G * d.S * x->nacc * 64);
+    rc |= dalloc(x, &d.xcnt, (size_t)d.RB * d.G * 32);
+    if (rc) { nmc_destroy(x); return rc; }
   }
   d.thin = 1; d.tune_interval = 100;
   HIPCHK(hipMemcpy(off, group_offsets, (n_groups + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
@@ -488,6 +523,9 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);
       HIPCHK(hipGetLastError());
       if (!partial) {
+        if (x->d.S > 1)   // row split: fresh exchange counters for the launch
+          HIPCHK(hipMemsetAsync(x->d.xcnt, 0, (size_t)x->d.RB * x->d.G * 32 * sizeof(unsigned),
+                                x->stream));
         if (int rc = launch_run(c0, c1, 0)) return rc;
       } else if (x->persistent) {
         HIPCHK(hipMemsetAsync(x->d.cnt, 0, (size_t)32 * 8 * x->d.RB * x->P * sizeof(unsigned),
@@ -627,6 +665,12 @@ int nmc_get_kernel_timing(nmc_ctx* x, double* step_ms, int64_t* step_n, int64_t*
   if (step_iters) *step_iters = x->step_iters;
   if (hyper_ms) *hyper_ms = x->hyper_ms;
   if (hyper_n) *hyper_n = x->hyper_n;
+  return 0;
+}
+
+int nmc_split_config(nmc_ctx* x, int* members, int* chain_blocks_per_launch) {
+  *members = x->d.S;
+  *chain_blocks_per_launch = x->d.S > 1 ? x->split_batch : x->d.RB;
   return 0;
 }
 

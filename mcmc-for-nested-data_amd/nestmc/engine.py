@@ -216,5 +216,8 @@ class Engine:
         w, cb, pe, cl, md = (ctypes.c_int() for _ in range(5))
         check(self.lib.nmc_launch_config(self.h, ctypes.byref(w), ctypes.byref(cb),
                                          ctypes.byref(pe), ctypes.byref(cl), ctypes.byref(md)))
+        sm, sb = ctypes.c_int(), ctypes.c_int()
+        check(self.lib.nmc_split_config(self.h, ctypes.byref(sm), ctypes.byref(sb)))
         return dict(waves_per_group=w.value, chain_blocks=cb.value, persistent=bool(pe.value),
-                    chains_per_block=cl.value, mode=MODE_NAMES.get(md.value, str(md.value)))
+                    chains_per_block=cl.value, mode=MODE_NAMES.get(md.value, str(md.value)),
+                    split_members=sm.value, chain_blocks_per_launch=sb.value)

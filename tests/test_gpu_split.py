@@ -1,0 +1,70 @@
+"""GPU: row-split none/complete pooling (reference CompletePooling
+posteriorSampling.py:662-685 -- every observation in ONE group, so one (chain, group)
+is a single workgroup's worth of chains over the whole dataset).
+
+Groups much larger than one workgroup's 64 KiB LDS row area are shared by S member
+workgroups (kernels.h nmc_split_exchange): each owns a contiguous row chunk, the
+members exchange their partial sums every step and all make the same decision.
+
+* complete pooling at n_total = 120 000 rows and none pooling with four 20 000-row
+  groups against the numpy oracle on the same Philox stream (flags exact, proposal LLs
+  within 1e-9 relative, recorded rows within 1e-9);
+* the split's order depends on (rows, fields, groups, CU count) only: two engines
+  holding halves of the chains, and chain blocks launched one per resident batch,
+  reproduce the one-engine run bit for bit.
+"""
+
+import numpy
+import pytest
+
+from gpu_cases import run_engine, run_oracle, synthetic
+from test_gpu_parity import _synthetic_state, close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("kind,C,G,N,n_iter", [
+    ("linreg_complete", 70, 1, 120000, 16),
+    ("regression3_none", 65, 4, 20000, 12),
+])
+def test_split_matches_oracle(gpu_lib, kind, C, G, N, n_iter):
+    fam, sizes, priors, pooling, names = synthetic(kind, C, G, N)
+    P = fam.n_params
+    st, nested = _synthetic_state(fam, sizes, priors, pooling, C, P, len(sizes))
+    seed = 4242
+    acc, llp, rows, cfg = run_engine(fam, sizes, st, numpy.arange(C), 11, n_iter, seed,
+                                     pooling=pooling, priors=priors, tune_interval=5)
+    assert cfg["split_members"] > 1, cfg
+    n = 3
+    oacc, ollp, orows, margin = run_oracle(nested, st, numpy.arange(n), numpy.arange(n) + 11,
+                                           n_iter, seed, pooling=pooling, priors=priors,
+                                           tune_interval=5)
+    bad = numpy.argwhere(acc[:n].astype(bool) != oacc)
+    assert bad.size == 0, "flag mismatch at %s (min decision margin %g)" % (bad[:5], margin)
+    assert close(llp[:n], ollp, rtol=1e-10)
+    assert close(rows[:n], orows)
+    assert acc.mean() > 0.02
+
+
+def test_split_shard_and_batch_invariance(gpu_lib):
+    fam, sizes, priors, pooling, names = synthetic("linreg_complete", 130, 1, 30000)
+    C, P = 130, fam.n_params
+    st, _ = _synthetic_state(fam, sizes, priors, pooling, C, P, 1)
+    args = dict(pooling=pooling, priors=priors, tune_interval=5)
+    whole = run_engine(fam, sizes, st, numpy.arange(C), 0, 10, 99, **args)
+    assert whole[3]["split_members"] > 1, whole[3]
+    lo = run_engine(fam, sizes, st, numpy.arange(0, 64), 0, 10, 99, **args)
+    hi = run_engine(fam, sizes, st, numpy.arange(64, C), 64, 10, 99, **args)
+    batched = run_engine(fam, sizes, st, numpy.arange(C), 0, 10, 99,
+                         env={"NMC_SPLIT_BATCH": "1"}, **args)
+    assert batched[3]["chain_blocks_per_launch"] == 1, batched[3]
+    for k in range(3):
+        merged = numpy.concatenate([lo[k], hi[k]], axis=0)
+        assert numpy.array_equal(merged, whole[k], equal_nan=True), k
+        assert numpy.array_equal(batched[k], whole[k], equal_nan=True), k
+    # the unsplit kernel sums in another order: same decisions, values within rounding
+    single = run_engine(fam, sizes, st, numpy.arange(C), 0, 10, 99, env={"NMC_SPLIT": "1"},
+                        **args)
+    assert single[3]["split_members"] == 1
+    assert numpy.array_equal(single[0], whole[0])
+    assert close(single[1], whole[1], rtol=1e-12) and close(single[2], whole[2], rtol=1e-12)

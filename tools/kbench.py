@@ -77,7 +77,7 @@ def run(kind, C, G, N, pooling, waves, iters, persist=None):
     eng.close()
     rate = C * G * iters / (ms / 1e3)
     return dict(kind=kind, C=C, G=G, N=N, pooling=pooling, waves=cfg["waves_per_group"],
-                persistent=cfg["persistent"],
+                persistent=cfg["persistent"], split_members=cfg["split_members"],
                 us_per_iter=ms * 1e3 / iters, wall_us_per_iter=wall * 1e6 / iters,
                 step_us_per_iter=kt["step_ms"] * 1e3 / max(1, kt["step_iters"]),
                 hyper_us=kt["hyper_ms"] * 1e3 / max(1, kt["hyper_launches"]),
@@ -89,7 +89,22 @@ def main():
     ap.add_argument("--iters", type=int, default=300)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="rows-per-group sweep (cost model)")
+    ap.add_argument("--complete", action="store_true",
+                    help="complete pooling at large n_total: row split vs one workgroup")
     a = ap.parse_args()
+    if a.complete:
+        for C, N in ((64, 100000), (256, 100000), (1024, 512000)):
+            for split in (None, "1"):
+                if split:
+                    os.environ["NMC_SPLIT"] = split
+                else:
+                    os.environ.pop("NMC_SPLIT", None)
+                iters = 40 if split else 200
+                r = run("linreg", C, 1, N, "complete", 0, iters)
+                r["split"] = "default" if split is None else split
+                print(json.dumps(r), flush=True)
+        os.environ.pop("NMC_SPLIT", None)
+        return
     if a.sweep:
         for rows in ("lds", "smem"):
             if rows == "smem":
