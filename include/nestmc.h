@@ -20,7 +20,16 @@
 #ifndef NESTMC_H
 #define NESTMC_H
 
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
+#else   /* hiprtc (runtime-compiled user families): its own fixed-width types */
+typedef __hip_internal::int64_t int64_t;
+typedef __hip_internal::uint64_t uint64_t;
+typedef __hip_internal::int32_t int32_t;
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::uint64_t uintptr_t;
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -39,6 +48,10 @@ enum { NMC_POOL_COMPLETE = 0, NMC_POOL_NONE = 1, NMC_POOL_PARTIAL = 2 };
  *   NMC_LL_GAUSS_MEAN obs = [m_0..m_{P-1}]; consts = {sd_0..sd_{P-1}}
  *   NMC_LL_LOGISTIC  obs = [x_1..x_k, y]; consts = {k, intercept}              */
 enum { NMC_LL_LINREG = 0, NMC_LL_GAUSS_MEAN = 1, NMC_LL_LOGISTIC = 2 };
+/* User families (the reference's arbitrary logLikelihoodFunction, :61-102, as device
+ * code): ids >= NMC_LL_USER_BASE come from nmc_user_family_compile; consts = the model's
+ * constants, passed to the user function as k.                                     */
+enum { NMC_LL_USER_BASE = 100 };
 
 /* prior families for none/complete pooling: scipy frozen distributions the
  * reference evaluates with .logpdf (posteriorSampling.py:293-294).
@@ -60,6 +73,18 @@ int nmc_device_count(int* n);
 /* Replaces the per-chain StepMethod construction (posteriorSampling.py:517-582,
  * :1146-1151): CSR offsets (:554-555), data, priors.  chain_base = global id of
  * local chain 0 (Philox key, posteriorSampling.py:225 seed = chain).           */
+/* Compile a user log-likelihood (hiprtc, gfx950) and register it as a family:
+ *   source defines  __device__ double nmc_user_loglik(const double* theta,  // [n_params]
+ *                                                     const double* row,    // [n_fields]
+ *                                                     const double* k);     // consts
+ * returning ONE observation's log-likelihood (the reference's logLikelihoodFunction,
+ * posteriorSampling.py:61-102, evaluated per row); include_dir = the library's csrc
+ * directory (kernels.h, fam_user.h).  *family_id -> pass as nmc_create's ll_family.
+ * Errors carry the compiler log (nmc_last_error).                                  */
+int nmc_user_family_compile(const char* source, int n_fields, int n_params,
+                            const char* include_dir, int* family_id);
+int nmc_user_family_shape(int family_id, int* n_fields, int* n_params);
+
 int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base,
                int n_groups, int n_params, int pooling, int ll_family,
                const double* ll_consts, int n_ll_consts,

@@ -56,6 +56,8 @@ struct nmc_ctx {
   int* gidx = nullptr;                    // [n_obs] group of each observation (obs-LL rows)
   int64_t nmax_group = 0;                 // rows of the largest group
   int split_batch = 0;                    // row split: chain blocks per (resident) launch
+  void* user = nullptr;                   // user family: its per-device kernel table (user.hip)
+  double* user_k = nullptr;               // user family: device copy of the model constants
 };
 
 static inline double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->d.vb0; }
@@ -84,6 +86,21 @@ static inline size_t run_lds_bytes(const nmc_ctx* x) {
   return lds_bytes_for(x, x->persistent && x->d.hlds ? 1 : 0, x->d.rows_lds);
 }
 
+// Resident blocks per CU to rely on, from the occupancy API's answer nb.  The API can
+// answer one block per CU too many where SGPRs bind (MI355X_MICROARCH.md, residency:
+// min(API, floor(800 / (ceil(sgpr / 16) * 16 + 16))) waves per SIMD); the step kernels use
+// <= 112 SGPRs -> 6 waves per SIMD, i.e. 24 / W blocks of W = 4k waves.  Other block
+// sizes keep one block of margin.
+static inline int nmc_safe_blocks(const nmc_ctx* x, int nb) {
+  const int W = x->d.W;
+  return W % 4 == 0 ? std::min(nb, 24 / W) : (nb > 1 ? nb - 1 : nb);
+}
+static inline size_t pair_lds_bytes(const nmc_ctx* x);
+// LDS of the persistent partial-pooling kernel (its occupancy query)
+static inline size_t nmc_persist_lds(const nmc_ctx* x) {
+  return x->d.pair ? pair_lds_bytes(x) : lds_bytes_for(x, x->d.hlds, x->d.rows_lds);
+}
+
 static inline int pop_event_pair(nmc_ctx* x, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v,
                                  size_t& used, std::pair<hipEvent_t, hipEvent_t>** out) {
   if (used == v.size()) {
@@ -93,6 +110,38 @@ static inline int pop_event_pair(nmc_ctx* x, std::vector<std::pair<hipEvent_t, h
     v.emplace_back(a, b);
   }
   *out = &v[used++];
+  return 0;
+}
+
+// The step-kernel launches of iterations [i0, i1): launch(mode, dev, grid, block, lds)
+// issues one kernel (built-in families: hipLaunchKernelGGL of the template instance;
+// user families: hipModuleLaunchKernel of the JIT module).  Row split: one launch per
+// resident batch of chain blocks.  Kernel timing events bracket the whole call.
+template <class Launch>
+static int nmc_run_launches(nmc_ctx* x, int i0, int i1, Launch&& launch) {
+  const Dev& d = x->d;
+  const size_t lds = run_lds_bytes(x);
+  std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
+  if (x->ktiming) {
+    if (int rc = pop_event_pair(x, x->kev, x->kev_used, &ev)) return rc;
+    if (x->kev_iters.size() < x->kev_used) x->kev_iters.resize(x->kev_used);
+    x->kev_iters[x->kev_used - 1] = i1 - i0;
+    HIPCHK(hipEventRecord(ev->first, x->stream));
+  }
+  const dim3 block(64 * d.W);
+  const int mode = run_mode(x);
+  if (mode == NMC_MODE_NOPOOL && d.S > 1) {   // row split: resident batches of chain blocks
+    for (int cb0 = 0; cb0 < d.RB; cb0 += x->split_batch) {
+      Dev db = d;
+      db.cb0 = cb0;
+      const int nb = std::min(x->split_batch, d.RB - cb0);
+      launch(mode, db, dim3(nb * d.G * d.S), block, lds);
+    }
+  } else {
+    launch(mode, d, dim3(d.RB * d.G * d.S), block, lds);
+  }
+  HIPCHK(hipGetLastError());
+  if (ev) HIPCHK(hipEventRecord(ev->second, x->stream));
   return 0;
 }
 
@@ -118,11 +167,16 @@ int nmc_call_linreg(nmc_ctx* x, NmcCall& c);
 int nmc_call_gauss_mean(nmc_ctx* x, NmcCall& c);
 int nmc_call_logistic(nmc_ctx* x, NmcCall& c);
 
+// user families (user.hip): runtime-compiled FamUser modules, ids >= NMC_LL_USER_BASE
+int nmc_call_user(nmc_ctx* x, NmcCall& c);
+int nmc_user_attach(nmc_ctx* x, int family);   // load the module on x's device, check shapes
+
 static inline int nmc_call_family(nmc_ctx* x, NmcCall& c) {
   switch (x->family) {
     case NMC_LL_LINREG: return nmc_call_linreg(x, c);
     case NMC_LL_GAUSS_MEAN: return nmc_call_gauss_mean(x, c);
     case NMC_LL_LOGISTIC: return nmc_call_logistic(x, c);
   }
+  if (x->family >= NMC_LL_USER_BASE) return nmc_call_user(x, c);
   return nmc_fail(-1, "unknown likelihood family");
 }

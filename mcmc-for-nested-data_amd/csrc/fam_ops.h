@@ -3,62 +3,42 @@
 #pragma once
 #include "ctx.h"
 
-// Iterations [i0, i1) of the step kernel (one launch).
+// Iterations [i0, i1) of the step kernel (one launch, or one per resident chain-block
+// batch under the row split).
 template <class Fam>
 static int nmc_launch_run(nmc_ctx* x, const Fam& fam, int i0, int i1, int flags) {
-  Dev& d = x->d;
-  const size_t lds = run_lds_bytes(x);
-  std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
-  if (x->ktiming) {
-    if (int rc = pop_event_pair(x, x->kev, x->kev_used, &ev)) return rc;
-    if (x->kev_iters.size() < x->kev_used) x->kev_iters.resize(x->kev_used);
-    x->kev_iters[x->kev_used - 1] = i1 - i0;
-    HIPCHK(hipEventRecord(ev->first, x->stream));
-  }
-  const dim3 grid(d.RB * d.G * d.S), block(64 * d.W);
-  switch (run_mode(x)) {
-    case NMC_MODE_NOPOOL:
-      if (d.S > 1) {   // row split: resident batches of chain blocks
-        for (int cb0 = 0; cb0 < d.RB; cb0 += x->split_batch) {
-          Dev db = d;
-          db.cb0 = cb0;
-          const int nb = std::min(x->split_batch, d.RB - cb0);
-          hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_NOPOOL>), dim3(nb * d.G * d.S), block, lds,
-                             x->stream, db, fam, d.obs, i0, i1, flags);
-        }
+  return nmc_run_launches(x, i0, i1, [&](int mode, const Dev& d, dim3 grid, dim3 block,
+                                         size_t lds) {
+    switch (mode) {
+      case NMC_MODE_NOPOOL:
+        hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_NOPOOL>), grid, block, lds, x->stream, d, fam,
+                           d.obs, i0, i1, flags);
         break;
-      }
-      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_NOPOOL>), grid, block, lds, x->stream, d, fam,
-                         d.obs, i0, i1, flags);
-      break;
-    case NMC_MODE_LAUNCH:
-      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_LAUNCH>), grid, block, lds, x->stream, d, fam,
-                         d.obs, i0, i1, flags);
-      break;
-    case NMC_MODE_SYNC:
-      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC>), grid, block, lds, x->stream, d, fam,
-                         d.obs, i0, i1, flags);
-      break;
-    case NMC_MODE_PAIR:
-      hipLaunchKernelGGL((nmc_k_pair<Fam>), grid, block, lds, x->stream, d, fam, d.obs, i0, i1,
-                         flags);
-      break;
-    case NMC_MODE_SYNC_REG:
-      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC_REG>), grid, block, lds, x->stream, d, fam,
-                         d.obs, i0, i1, flags);
-      break;
-    default:
-      hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC_LDS>), grid, block, lds, x->stream, d, fam,
-                         d.obs, i0, i1, flags);
-  }
-  HIPCHK(hipGetLastError());
-  if (ev) HIPCHK(hipEventRecord(ev->second, x->stream));
-  return 0;
+      case NMC_MODE_LAUNCH:
+        hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_LAUNCH>), grid, block, lds, x->stream, d, fam,
+                           d.obs, i0, i1, flags);
+        break;
+      case NMC_MODE_SYNC:
+        hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC>), grid, block, lds, x->stream, d, fam,
+                           d.obs, i0, i1, flags);
+        break;
+      case NMC_MODE_PAIR:
+        hipLaunchKernelGGL((nmc_k_pair<Fam>), grid, block, lds, x->stream, d, fam, d.obs, i0, i1,
+                           flags);
+        break;
+      case NMC_MODE_SYNC_REG:
+        hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC_REG>), grid, block, lds, x->stream, d,
+                           fam, d.obs, i0, i1, flags);
+        break;
+      default:
+        hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC_LDS>), grid, block, lds, x->stream, d,
+                           fam, d.obs, i0, i1, flags);
+    }
+  });
 }
 
 // Partial pooling: may every workgroup of the grid be resident at once?  (The
-// persistent kernel's chain-block waits need it.)  One block of margin per CU where
-// the occupancy query can over-report (MI355X_MICROARCH.md, residency).
+// persistent kernel's chain-block waits need it.)
 template <class Fam>
 static bool nmc_can_persist(nmc_ctx* x) {
   if (const char* e = getenv("NMC_PERSIST")) return atoi(e) != 0;
@@ -67,17 +47,10 @@ static bool nmc_can_persist(nmc_ctx* x) {
                   : !x->d.hlds ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC>
                   : x->d.hreg  ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_REG>
                                : (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_LDS>;
-  const size_t lds = x->d.pair ? pair_lds_bytes(x) : lds_bytes_for(x, x->d.hlds, x->d.rows_lds);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W, lds) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W, nmc_persist_lds(x)) !=
       hipSuccess)
     return false;
-  // The API can answer one block per CU too many where SGPRs bind (MI355X_MICROARCH.md,
-  // residency: min(API, floor(800 / (ceil(sgpr / 16) * 16 + 16))) waves per SIMD); the
-  // step kernels use <= 112 SGPRs -> 6 waves per SIMD, i.e. 24 / W blocks of W = 4k waves.
-  // Other block sizes keep one block of margin.
-  const int W = x->d.W;
-  const int safe = W % 4 == 0 ? std::min(nb, 24 / W) : (nb > 1 ? nb - 1 : nb);
-  return (int64_t)x->d.RB * x->d.G <= (int64_t)safe * x->ncu;
+  return (int64_t)x->d.RB * x->d.G <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
 }
 
 template <class Fam>
@@ -93,9 +66,7 @@ static int nmc_fam_call(nmc_ctx* x, const Fam& fam, NmcCall& c) {
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, nmc_k_run<Fam, NMC_MODE_NOPOOL>,
                                                        64 * x->d.W, run_lds_bytes(x)) != hipSuccess)
         return nmc_fail(-2, "occupancy query failed");
-      const int W = x->d.W;
-      const int safe = W % 4 == 0 ? std::min(nb, 24 / W) : (nb > 1 ? nb - 1 : nb);
-      c.result = safe * x->ncu;
+      c.result = nmc_safe_blocks(x, nb) * x->ncu;
       return 0;
     }
     case NMC_OP_GROUP_LL: {

@@ -15,8 +15,10 @@
 // Algebra is restructured (e.g. sum r^2 then scale once) but no fast-math: NaN and
 // inf propagate exactly as the reference's MH branches (:347-367) need.
 #pragma once
+#ifndef __HIPCC_RTC__   // (hiprtc, user families: the runtime provides these)
 #include <hip/hip_runtime.h>
 #include <math.h>
+#endif
 
 #include "special.h"
 

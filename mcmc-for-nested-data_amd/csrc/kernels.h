@@ -37,8 +37,10 @@
 //     boundary publishes, plain loads read.
 // Every spin is bounded: a timeout sets d.tmo and every workgroup drains.
 #pragma once
+#ifndef __HIPCC_RTC__   // (hiprtc, user families: the runtime provides these)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "families.h"
 #include "rng.h"

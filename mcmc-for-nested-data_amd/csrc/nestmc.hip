@@ -93,7 +93,7 @@ static void choose_geometry(nmc_ctx* x) {
   // (measured on MI355X at cfg 3: 8.6-9.8 us per iteration against 8.0 for SYNC_REG --
   // the three-sum pass is VALU-bound with two of the four SIMDs holding a Gibbs wave --
   // so it is opt-in, NMC_PAIR=1, for the measurements in DESIGN.md)
-  d.pair = d.hreg && d.P == 2 && d.rows_lds &&
+  d.pair = d.hreg && d.P == 2 && d.rows_lds && x->family < NMC_LL_USER_BASE &&
            (size_t)nmc_pair_lds(x->nacc, d.nmax * x->nf).total * 512 <= (size_t)160 * 1024 &&
            getenv("NMC_PAIR") && atoi(getenv("NMC_PAIR"));
   if (d.pair && d.W < 4) d.W = 4;
@@ -187,6 +187,14 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   }
   if (ll_family == NMC_LL_LOGISTIC && (n_fields - 1) + (int)ll_consts[1] != n_params)
     return fail(-1, "logistic: n_params != k + intercept");
+  if (ll_family >= NMC_LL_USER_BASE) {
+    int unf = 0, unp = 0;
+    if (int rc0 = nmc_user_family_shape(ll_family, &unf, &unp)) return rc0;
+    if (unf != n_fields || unp != n_params)
+      return fail(-1, "user family compiled for other n_fields / n_params");
+  } else if (ll_family < 0 || ll_family > NMC_LL_LOGISTIC) {
+    return fail(-1, "unknown likelihood family");
+  }
 
   nmc_ctx* x = new nmc_ctx();
   x->device = device;
@@ -240,6 +248,13 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
       x->ncu = prop.multiProcessorCount;
   }
   x->nacc = ll_family == NMC_LL_GAUSS_MEAN ? n_fields : 1;
+  if (ll_family >= NMC_LL_USER_BASE) {   // runtime-compiled family: module + constants
+    if (int rc0 = nmc_user_attach(x, ll_family)) { nmc_destroy(x); return rc0; }
+    if (n_ll_consts > 0) {
+      if (int rc0 = dalloc(x, &x->user_k, (size_t)n_ll_consts)) { nmc_destroy(x); return rc0; }
+      HIPCHK(hipMemcpy(x->user_k, ll_consts, (size_t)n_ll_consts * 8, hipMemcpyHostToDevice));
+    }
+  }
   // numpy pairwise-sum plan of the hyper update (partial pooling)
   std::vector<int> starts, merges;
   pairwise_plan(0, n_groups, starts, merges);

@@ -13,8 +13,10 @@
 //   normal = sqrt(-2 log(1-ua)) * cos(2 pi ub)          (Box-Muller, cos branch)
 // Compiled with -ffp-contract=off: every expression rounds exactly as written.
 #pragma once
+#ifndef __HIPCC_RTC__   // (hiprtc, user families: the runtime provides these)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #define NMC_HD __host__ __device__ __forceinline__
 

@@ -10,9 +10,11 @@
 // * nmc_pairwise_sum : numpy's float64 add.reduce order (numpy.mean / numpy.sum of
 //   posteriorSampling.py:485, :494), so hyper means match the reference bit for bit.
 #pragma once
+#ifndef __HIPCC_RTC__   // (hiprtc, user families: the runtime provides these)
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#endif
 
 #include "../../include/nestmc.h"
 

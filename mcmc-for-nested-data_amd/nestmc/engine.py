@@ -48,7 +48,7 @@ class Engine:
         h = ctypes.c_void_p()
         check(lib.nmc_create(
             ctypes.byref(h), self.device, self.C, self.chain_base, self.G, self.P,
-            _lib.POOLING[pooling], _lib.FAMILY[family.family], dptr(consts), len(consts),
+            _lib.POOLING[pooling], family.family_id(), dptr(consts), len(consts),
             self.off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), dptr(obs),
             obs.shape[0], obs.shape[1],
             None if pfam is None else pfam.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),

@@ -14,8 +14,9 @@ observation.  On the GPU the likelihood must be a known device functor
   evaluates exactly what the reference would.
 
 Families: ``LinearRegression`` (example/regression.py:53-67, and the cfg 3/4 model
-with known noise sd), ``GaussianMean`` (example/distribution.py:18-24) and
-``Logistic`` (cfg 5).
+with known noise sd), ``GaussianMean`` (example/distribution.py:18-24),
+``Logistic`` (cfg 5), and ``DeviceLikelihood``: any per-observation log-likelihood
+written as a HIP device function, compiled for gfx950 at run time (csrc/user.hip).
 """
 
 import numpy
@@ -36,6 +37,11 @@ class Family:
 
     def bytes_per_obs(self):
         return 8 * self.n_fields
+
+    def family_id(self):
+        """The C-ABI ll_family code of this family (nmc_create)."""
+        from . import _lib
+        return _lib.FAMILY[self.family]
 
     def __call__(self, parameter):
         raise NotImplementedError
@@ -164,6 +170,80 @@ class Logistic(Family):
         theta = numpy.vstack(parameter).T
         eta = numpy.sum(self.X * theta, axis=1)
         return self.y * eta - numpy.logaddexp(0.0, eta)
+
+
+_USER_IDS = {}   # (source, n_fields, n_params) -> registered family id (per process)
+
+
+class DeviceLikelihood(Family):
+    """A user log-likelihood as device code: the GPU form of the reference's arbitrary
+    ``logLikelihoodFunction`` (posteriorSampling.py:61-102).
+
+    ``source`` defines one observation's log-likelihood::
+
+        __device__ double nmc_user_loglik(const double* theta,  // [n_params]
+                                          const double* row,    // [n_fields]
+                                          const double* k)      // consts
+        { ... }
+
+    ``obs`` is the (n_obs, n_fields) table of observations in the reference's response
+    order (``row`` is one of its rows) and ``consts`` the model's constants.  The source
+    is compiled with hiprtc for gfx950 the first time an engine uses it (csrc/user.hip,
+    the library's own flags: IEEE fp64, no contraction), then cached for the process.
+    The kernels sum the per-row values in the same fixed order as the built-in families.
+
+    ``host_function(parameter[P][n]) -> ll[n]`` (optional) is the same model in the
+    reference's calling convention; the host needs it only for ``startWithMLE`` (the
+    Nelder-Mead objective, :1102-1141) -- every other evaluation runs on the device.
+    """
+
+    family = "user"
+
+    def __init__(self, obs, source, n_params, consts=(), host_function=None):
+        obs = numpy.asarray(obs, dtype=numpy.float64)
+        if obs.ndim == 1:
+            obs = obs[:, None]
+        if obs.ndim != 2:
+            raise ValueError("obs must be (n_obs, n_fields)")
+        self._obs = numpy.ascontiguousarray(obs)
+        self.n_fields = self._obs.shape[1]
+        self.n_params = int(n_params)
+        if not 1 <= self.n_params <= 16:
+            raise ValueError("1 <= n_params <= 16")
+        if "nmc_user_loglik" not in source:
+            raise ValueError("source must define __device__ double nmc_user_loglik(...)")
+        self.source = source
+        self._consts = [float(v) for v in consts]
+        self.host_function = host_function
+
+    def family_id(self):
+        import ctypes
+        import os
+        from . import _lib
+        key = (self.source, self.n_fields, self.n_params)
+        if key not in _USER_IDS:
+            lib = _lib.load()
+            inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                               "csrc")
+            fid = ctypes.c_int(-1)
+            _lib.check(lib.nmc_user_family_compile(self.source.encode(), self.n_fields,
+                                                   self.n_params, inc.encode(),
+                                                   ctypes.byref(fid)))
+            _USER_IDS[key] = fid.value
+        return _USER_IDS[key]
+
+    def obs(self):
+        return self._obs
+
+    def consts(self):
+        return list(self._consts)
+
+    def __call__(self, parameter):
+        if self.host_function is None:
+            raise TypeError("DeviceLikelihood: no host_function given; host-side evaluation "
+                            "(startWithMLE's Nelder-Mead objective) needs the model in the "
+                            "reference's calling convention")
+        return self.host_function(parameter)
 
 
 def is_family(obj):

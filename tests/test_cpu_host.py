@@ -118,3 +118,26 @@ def test_batched_init_matches_reference_order(name):
         if c.pooling == "partial":
             assert numpy.array_equal(st["mu"][ch], o.mu[0])
             assert numpy.array_equal(st["s2"][ch], o.s2[0])
+
+
+def test_user_family_compiles_without_gpu():
+    """hiprtc compiles a user log-likelihood for gfx950 on the host (no device needed);
+    a broken source surfaces the compiler log; the host callable is optional."""
+    import user_models
+    from nestmc import _lib
+    from nestmc.families import DeviceLikelihood
+    fam = DeviceLikelihood(numpy.zeros((10, 3)), user_models.POISSON, 2, consts=[0.1])
+    fid = fam.family_id()
+    assert fid >= 100
+    assert fam.family_id() == fid            # cached per process
+    lib = _lib.load()
+    import ctypes
+    nf, npar = ctypes.c_int(), ctypes.c_int()
+    assert lib.nmc_user_family_shape(fid, ctypes.byref(nf), ctypes.byref(npar)) == 0
+    assert (nf.value, npar.value) == (3, 2)
+    bad = DeviceLikelihood(numpy.zeros((10, 2)), "__device__ double nmc_user_loglik("
+                           "const double* t, const double* r, const double* k) { return q; }", 2)
+    with pytest.raises(_lib.NestmcError, match="q"):
+        bad.family_id()
+    with pytest.raises(TypeError):
+        fam([numpy.zeros(10), numpy.zeros(10)])
