@@ -180,6 +180,12 @@ int nmc_write_ll_csv(const char* path, int append, const double* ll, int64_t n,
 
 /* Multi-GPU (replaces the process-per-chain fan-out, posteriorSampling.py:182-201):
  * RCCL communicator over xGMI and ONE gather of every rank's sample store.    */
+/* Diagnostic._computeVariogram (sampleDiagnosis.py:189-194) for every lag: x = [K][m][n]
+ * (K columns, m half-chains of n samples, host memory), out = [K][n] with
+ * out[k][t] = sum_j sum_{i>=t} (x[k][j][i] - x[k][j][i-t])^2 / (m (n - t)), the
+ * reference's summation order; runs on `device`; n <= 8192.                          */
+int nmc_variogram(int device, const double* x, int K, int m, int n, double* out);
+
 int nmc_comm_unique_id(unsigned char* out /* 128 bytes */);
 int nmc_comm_init(void** comm, const unsigned char* id, int nranks, int rank, int device);
 int nmc_comm_destroy(void* comm);

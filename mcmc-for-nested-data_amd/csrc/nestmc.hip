@@ -299,7 +299,7 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
                                     std::max<int64_t>(1, x->ncu / n_groups)});
     if (const char* e = getenv("NMC_SPLIT")) {
       const int v = atoi(e);
-      if (v >= 1 && v <= 64) d.S = v;
+      if (v >= 1 && v <= 256) d.S = v;
     }
   }
   d.nmax = (int)((nmax + d.S - 1) / d.S);   // rows of the largest member

@@ -65,6 +65,8 @@ SIGNATURES = {
     "nmc_get_kernel_timing": (ctypes.c_int, [_vp, _c_double_p, _c_int64_p, _c_int64_p,
                                              _c_double_p, _c_int64_p]),
     "nmc_split_config": (ctypes.c_int, [_vp, _c_int_p, _c_int_p]),
+    "nmc_variogram": (ctypes.c_int, [ctypes.c_int, _c_double_p, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, _c_double_p]),
     "nmc_user_family_compile": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_char_p, _c_int_p]),
     "nmc_user_family_shape": (ctypes.c_int, [ctypes.c_int, _c_int_p, _c_int_p]),

@@ -93,13 +93,18 @@ def main():
                     help="complete pooling at large n_total: row split vs one workgroup")
     a = ap.parse_args()
     if a.complete:
-        for C, N in ((64, 100000), (256, 100000), (1024, 512000)):
-            for split in (None, "1"):
+        cases = [(C, N, sp) for C, N in ((64, 100000), (256, 100000), (1024, 512000))
+                 for sp in (None, "1")]
+        if os.environ.get("KB_SPLITS"):   # explicit member counts (diagnostics)
+            cases = [(int(C), int(N), sp) for C, N, sp in
+                     (t.split(":") for t in os.environ["KB_SPLITS"].split(","))]
+        for C, N, split in cases:
+            if True:
                 if split:
                     os.environ["NMC_SPLIT"] = split
                 else:
                     os.environ.pop("NMC_SPLIT", None)
-                iters = 40 if split else 200
+                iters = 40 if split == "1" else 200
                 r = run("linreg", C, 1, N, "complete", 0, iters)
                 r["split"] = "default" if split is None else split
                 print(json.dumps(r), flush=True)
