@@ -66,7 +66,8 @@ static inline size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
   const Dev& d = x->d;
   // (register hand-off: no LDS payload buffers)
   return (size_t)nmc_lds(x->nacc, d.P, x->pooling == NMC_POOL_PARTIAL, d.nleaf, d.ntail, d.W,
-                         d.G, hlds && !d.hreg, rows_lds ? d.nmax * x->nf : 0)
+                         d.G, hlds && !d.hreg,
+                         rows_lds ? d.nmax * x->nf : nmc_stage_doubles(x->nf, d.W))
              .total * 512;
 }
 static inline size_t pair_lds_bytes(const nmc_ctx* x) {
@@ -130,7 +131,7 @@ static int nmc_run_launches(nmc_ctx* x, int i0, int i1, Launch&& launch) {
   }
   const dim3 block(64 * d.W);
   const int mode = run_mode(x);
-  if (mode == NMC_MODE_NOPOOL && d.S > 1) {   // row split: resident batches of chain blocks
+  if (d.S > 1) {   // row split: resident batches of chain blocks
     for (int cb0 = 0; cb0 < d.RB; cb0 += x->split_batch) {
       Dev db = d;
       db.cb0 = cb0;

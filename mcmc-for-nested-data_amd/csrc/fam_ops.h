@@ -50,7 +50,7 @@ static bool nmc_can_persist(nmc_ctx* x) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W, nmc_persist_lds(x)) !=
       hipSuccess)
     return false;
-  return (int64_t)x->d.RB * x->d.G <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
+  return (int64_t)x->d.RB * x->d.G * x->d.S <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
 }
 
 template <class Fam>
@@ -61,10 +61,16 @@ static int nmc_fam_call(nmc_ctx* x, const Fam& fam, NmcCall& c) {
     case NMC_OP_CAN_PERSIST:
       c.result = nmc_can_persist<Fam>(x) ? 1 : 0;
       return 0;
-    case NMC_OP_CAPACITY: {   // resident none/complete step-kernel workgroups (safe count)
+    case NMC_OP_CAPACITY: {   // resident step-kernel workgroups of the run mode (safe count)
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, nmc_k_run<Fam, NMC_MODE_NOPOOL>,
-                                                       64 * x->d.W, run_lds_bytes(x)) != hipSuccess)
+      const int mode = run_mode(x);
+      const void* k = mode == NMC_MODE_NOPOOL   ? (const void*)nmc_k_run<Fam, NMC_MODE_NOPOOL>
+                      : mode == NMC_MODE_SYNC   ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC>
+                      : mode == NMC_MODE_SYNC_REG ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_REG>
+                      : mode == NMC_MODE_SYNC_LDS ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_LDS>
+                                                  : (const void*)nmc_k_run<Fam, NMC_MODE_LAUNCH>;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W, run_lds_bytes(x)) !=
+          hipSuccess)
         return nmc_fail(-2, "occupancy query failed");
       c.result = nmc_safe_blocks(x, nb) * x->ncu;
       return 0;

@@ -791,6 +791,88 @@ __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename F
   for (int k = 0; k < Fam::NACC; ++k) acc[k] = (a[0][k] + a[1][k]) + (a[2][k] + a[3][k]);
 }
 
+// ---------------------------------------------------------------------------
+// Rows that do not fit LDS (groups over 64 KiB): each wave stages its tile through two
+// private LDS buffers of NMC_SR(NF) rows, copied by LDS-DMA (global_load_lds_dwordx4, no
+// registers) one chunk ahead of the chunk it computes, so the row fetch -- an L2 / MALL
+// round trip per row for the scalar-load loop it replaces -- hides behind the arithmetic.
+// Same R-row blocks, accumulators and order as nmc_ll_rows (bit-identical sums).
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int nmc_row_block(int nf) { return (16 / nf) > 0 ? 16 / nf : 1; }
+// rows per chunk: as many whole row blocks as one 1 KiB DMA instruction carries beside
+// 16 B of alignment slack (n_fields <= 64: at least one row)
+__host__ __device__ constexpr int nmc_stage_rows(int nf) {
+  return (1008 / (nf * 8)) / nmc_row_block(nf) > 0
+             ? nmc_row_block(nf) * ((1008 / (nf * 8)) / nmc_row_block(nf))
+             : nmc_row_block(nf);
+}
+// one buffer: the chunk's doubles plus 16 B of alignment slack, in whole 1 KiB DMAs
+__host__ __device__ constexpr int nmc_stage_buf(int nf) {
+  return ((nmc_stage_rows(nf) * nf + 2) * 8 + 1023) / 1024 * 128;
+}
+__host__ __device__ constexpr int nmc_stage_doubles(int nf, int W) { return W * 2 * nmc_stage_buf(nf); }
+
+template <class Fam>
+__device__ __forceinline__ void nmc_ll_rows_staged(const Fam& fam, const typename Fam::Reg& reg,
+                                                   const double* __restrict__ p, int n,
+                                                   const double* lim, double* stage,
+                                                   double (&acc)[Fam::NACC]) {
+  constexpr int NF = Fam::NFIELDS;
+  constexpr int R = nmc_row_block(NF);
+  constexpr int SR = nmc_stage_rows(NF);
+  constexpr int BUF = nmc_stage_buf(NF);        // doubles per buffer
+  constexpr int K = BUF / 128;                  // 1 KiB DMA instructions per chunk
+  static_assert(K >= 1 && K <= 15, "vmcnt immediate");
+  const int lane = threadIdx.x & 63;
+  double a[4][Fam::NACC];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int k = 0; k < Fam::NACC; ++k) a[s][k] = 0.0;
+  const uintptr_t last = ((uintptr_t)lim - 16) & ~(uintptr_t)15;   // last whole 16 B of the group
+  auto issue = [&](int c, double* buf) -> int {   // chunk c -> buf; returns its offset (doubles)
+    const uintptr_t src = (uintptr_t)(p + (size_t)c * SR * NF);
+    const uintptr_t a16 = src & ~(uintptr_t)15;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the buffer's last reads are done
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+      uintptr_t g = a16 + (uintptr_t)(q * 64 + lane) * 16;
+      g = g > last ? (last > a16 ? last : a16) : g;      // never past the group's rows
+      __builtin_amdgcn_global_load_lds((nmc_glb_ptr)g, (nmc_lds_ptr)(buf + q * 128), 16, 0, 0);
+    }
+    return (int)((src - a16) / 8);
+  };
+  const int nch = (n + SR - 1) / SR;
+  int off_cur = nch > 0 ? issue(0, stage) : 0;
+  for (int c = 0; c < nch; ++c) {
+    double* cur = stage + (c & 1) * BUF;
+    int off_next = 0;
+    if (c + 1 < nch) {
+      off_next = issue(c + 1, stage + ((c + 1) & 1) * BUF);
+      // chunk c has landed once at most chunk c+1's K copies are outstanding (loads return
+      // in order); vmcnt field [3:0], expcnt / lgkmcnt left unconstrained
+      __builtin_amdgcn_s_waitcnt((K & 15) | (7 << 4) | (15 << 8));
+    } else {
+      __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const double* q = cur + off_cur;
+    const int rows = n - c * SR < SR ? n - c * SR : SR;
+    const int nb = rows / R;
+    for (int b = 0; b < nb; ++b) {
+      double v[R * NF];
+#pragma unroll
+      for (int j = 0; j < R * NF; ++j) v[j] = q[(size_t)b * (R * NF) + j];
+      fam.template accumN<R>(reg, v, a);
+    }
+    for (int r = nb * R; r < rows; ++r) fam.accum(reg, q + (size_t)r * NF, a[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    off_cur = off_next;
+  }
+#pragma unroll
+  for (int k = 0; k < Fam::NACC; ++k) acc[k] = (a[0][k] + a[1][k]) + (a[2][k] + a[3][k]);
+}
+
 // The tile partials of one sum in a fixed order: tile k into accumulator k % 4, combined
 // (a0+a1)+(a2+a3); every LDS read in flight at once (slots past the last tile hold -0.0,
 // and x + (-0.0) == x).
@@ -1202,6 +1284,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const int g = (b / S) % G, cb = (b / S) / G + d.cb0;
   const int c = nmc_lane_chain(d, cb, lane);
   const bool live = nmc_lane_owns(d, c, lane) && mb == 0;   // member 0 writes the outputs
+  const bool g0w = g == 0 && mb == 0;   // writes the chain block's hyper-parameters
   const int cc = c < C ? c : C - 1;
   constexpr bool sync =
       MODE == NMC_MODE_SYNC || MODE == NMC_MODE_SYNC_LDS || MODE == NMC_MODE_SYNC_REG;
@@ -1213,7 +1296,9 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   // counter add, poll -- is behind a whole step) and the priors that need it come from
   // the Gibbs wave when it lands in the step that uses it (P <= 2)
   const int lag = hr && P >= 2 ? 2 : 1;
-  const int row_doubles = d.rows_lds ? d.nmax * Fam::NFIELDS : 0;
+  // rows in LDS for the launch, or every wave's two staging buffers (nmc_ll_rows_staged)
+  const int row_doubles =
+      d.rows_lds ? d.nmax * Fam::NFIELDS : nmc_stage_doubles(Fam::NFIELDS, blockDim.x >> 6);
   const nmc_lds_layout L =
       nmc_lds(Fam::NACC, P, PARTIAL, d.nleaf, d.ntail, W, G, hl && !hr ? 1 : 0, row_doubles);
   double* th = lds + L.th * 64 + lane;            // th[p * 64]: this lane's chain, parameter p
@@ -1228,6 +1313,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const nmc_tiling TI = nmc_tiles(nrow, d.tile);
   const int nt = TI.nt;
   const double* grows = obs + r0 * Fam::NFIELDS;
+  const double* glim = obs + d.off[g + 1] * Fam::NFIELDS;   // end of the group's rows
   const size_t PGC = (size_t)P * G * C;
   const size_t gc = (size_t)g * C + cc;
   const bool ctl = w == 0;
@@ -1364,8 +1450,9 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       if (done) {
       } else if (d.rows_lds) {   // wave-uniform LDS address: broadcast ds_reads, pipelined
         nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
-      } else {          // wave-uniform global address: scalar loads
-        nmc_ll_rows(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, acc);
+      } else {          // rows beyond LDS: staged per wave by LDS-DMA, two chunks deep
+        nmc_ll_rows_staged(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, glim,
+                           lrows + (size_t)w * 2 * nmc_stage_buf(Fam::NFIELDS), acc);
       }
 #pragma unroll
       for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = acc[j];
@@ -1399,7 +1486,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             nmc_drain_vm();
             if (p == 0) NMC_STAMP_AUX(t, 14);
 #endif
-            nmc_hyper_compute_reg(d, cb, kt, kq, lds, L.hyp, g == 0, fz, fx, xv);
+            nmc_hyper_compute_reg(d, cb, kt, kq, lds, L.hyp, g0w, fz, fx, xv);
             if (p == 0) NMC_STAMP_AUX(t, 15);
             if (P <= 2) {   // the update lands in the step that needs it: this step's priors
               const int sp = gs & 1;
@@ -1425,7 +1512,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     }
     // closing: tasks ge-lag .. ge-1 (group-0 workgroups write and record them); the same
     // barrier as the other waves' nmc_wait_published
-    if (ok && g == 0) {
+    if (ok && g0w) {
       const int ge = i1 * P;
       if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L)) {
         for (int k = ge - lag > gs0 ? ge - lag : gs0; k < ge; ++k) {
@@ -1489,13 +1576,13 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
               nmc_hyper_load(d, src, aq, cc, 0, G, lds, L, 0);
               asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
-            nmc_hyper_compute(d, cb, atq, aq, lds, L, g == 0, hz, hx, 0);
+            nmc_hyper_compute(d, cb, atq, aq, lds, L, g0w, hz, hx, 0);
             upd = true;
           }
         } else if (comp_now) {   // P >= 2: task gs-2, copied into buffer (gs-2)&1 at step gs-1
           const size_t hvi = (((size_t)(ctq - d.vbase) * P + cq) * C + cc) * 2;
           if (p == 0) NMC_STAMP_CMP(t, 13);
-          nmc_hyper_compute(d, cb, ctq, cq, lds, L, g == 0, d.vh[hvi], d.vh[hvi + 1],
+          nmc_hyper_compute(d, cb, ctq, cq, lds, L, g0w, d.vh[hvi], d.vh[hvi + 1],
                             (gs & 1) * (G + 1));
           if (p == 0) NMC_STAMP_CMP(t, 14);
           upd = post_prior;
@@ -1620,9 +1707,9 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         if constexpr (sync) {   // every parameter of t-1 is published once P-1's count is full
           ok = nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(t - i0), lds, L);
           if (!ok) break;
-          nmc_hyper<NMC_SRC_SC1>(d, ((t - 1) & 1) ? d.vb1 : d.vb0, cb, t - 1, lds, L, g == 0);
+          nmc_hyper<NMC_SRC_SC1>(d, ((t - 1) & 1) ? d.vb1 : d.vb0, cb, t - 1, lds, L, g0w);
         } else {
-          nmc_hyper<NMC_SRC_GLOBAL>(d, ((t - 1) & 1) ? d.vb1 : d.vb0, cb, t - 1, lds, L, g == 0);
+          nmc_hyper<NMC_SRC_GLOBAL>(d, ((t - 1) & 1) ? d.vb1 : d.vb0, cb, t - 1, lds, L, g0w);
         }
         if (ctl) {
           const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
@@ -1642,7 +1729,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         for (int j = 0; j < Fam::NACC; ++j) {
           acc[j] = nmc_sum_slots(lds + (L.part + j * NMC_NSLOT) * 64 + lane);
         }
-        if constexpr (!PARTIAL) if (S > 1)   // row split: every member's partials, in order
+        if (S > 1)   // row split: every member's partials, in member order
           nmc_split_exchange(d, cb, g, mb, t * P + p - i0 * P, acc);
         if (p == 0) NMC_STAMP(t, 10);
         double thp[Fam::MAXP];
@@ -1670,7 +1757,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
           if (live)
             __hip_atomic_store(((t & 1) ? d.vb1 : d.vb0) + (size_t)p * G * C + gc, vn,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          pub_p = p;
+          if (mb == 0) pub_p = p;   // (row split: member 0 publishes and counts)
         }
         st[(NMC_ST_S * P + p) * 64] = accept ? c_sA : c_sR;
         q_acc = accept;
@@ -1716,7 +1803,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     d.ll[gc] = c_LL;
   }
   // ---- closing Gibbs updates after i1-1 (group-0 workgroups write and record them) ----
-  if constexpr (hl) if (ok && g == 0) {
+  if constexpr (hl) if (ok && g0w) {
     const int ge = i1 * P;   // tasks ge-2 (copied at the last step; P >= 2) and ge-1 are left
     if (!hr && P >= 2 && gw) {
       const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 2)) * C + cc) * 2;
@@ -1739,7 +1826,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       nmc_hyper_compute(d, cb, i1 - 1, P - 1, lds, L, true, d.vh[hvi], d.vh[hvi + 1], ho);
     }
   }
-  if constexpr (sync && !hl) if (ok && g == 0) {
+  if constexpr (sync && !hl) if (ok && g0w) {
     nmc_hyper_sdm(d, lds, L, lane);
     nmc_hyper_variates(d, cb, i1 - 1, lds, L, 0, W);
     nmc_drain_vm();

@@ -217,7 +217,7 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   int* pf = nullptr;
   double* pp = nullptr;
   rc |= dalloc(x, &off, n_groups + 1);
-  rc |= dalloc(x, &dobs, (size_t)n_obs * n_fields);
+  rc |= dalloc(x, &dobs, (size_t)n_obs * n_fields + 4);   // (+32 B: staged-row DMA slack)
   rc |= dalloc(x, &pf, n_params);
   rc |= dalloc(x, &pp, (size_t)8 * n_params);
   // (+72 C + 128 slack: the Gibbs wave reads 72 groups' values unconditionally, and the
@@ -286,13 +286,13 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   for (int g = 0; g < n_groups; ++g)
     nmax = std::max<int64_t>(nmax, group_offsets[g + 1] - group_offsets[g]);
   x->nmax_group = nmax;
-  // Row split (none/complete pooling): groups far larger than one workgroup's 64 KiB LDS
-  // row area are shared by S workgroups, at most 64 and at most one per CU per group.
-  // S depends on (rows, fields, groups, CU count) only -- never on the chain count -- so
-  // the partial-sum order, and every result, is the same whatever the sharding.
+  // Row split: groups far larger than one workgroup's 64 KiB LDS row area are shared by S
+  // workgroups, at most 64 and at most one per CU per group.  S depends on (rows,
+  // fields, groups, CU count) only -- never on the chain count -- so the partial-sum
+  // order, and every result, is the same whatever the sharding or launch batching.
   d.S = 1;
   d.cb0 = 0;
-  if (pooling != NMC_POOL_PARTIAL) {
+  {
     const int64_t target = std::max<int64_t>(256, (64 * 1024) / (n_fields * 8));
     if (nmax > 2 * target)
       d.S = (int)std::min<int64_t>({64, (nmax + target - 1) / target,
@@ -313,7 +313,9 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     NmcCall c;
     c.op = NMC_OP_CAN_PERSIST;
     if (int rc2 = nmc_call_family(x, c)) { nmc_destroy(x); return rc2; }
-    x->persistent = c.result == 1;
+    // row split: always persistent (the members exchange every step), in resident batches
+    // of chain blocks when the whole grid is not (chain blocks are independent)
+    x->persistent = c.result == 1 || d.S > 1;
   }
   if (d.S > 1) {   // row split: resident batches of chain blocks, exchange buffers
     NmcCall c;
@@ -545,6 +547,9 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       } else if (x->persistent) {
         HIPCHK(hipMemsetAsync(x->d.cnt, 0, (size_t)32 * 8 * x->d.RB * x->P * sizeof(unsigned),
                               x->stream));
+        if (x->d.S > 1)
+          HIPCHK(hipMemsetAsync(x->d.xcnt, 0, (size_t)x->d.RB * x->d.G * 32 * sizeof(unsigned),
+                                x->stream));
         if (int rc = launch_run(c0, c1, NMC_RUN_HYPER_LOAD)) return rc;
       } else {
         for (int it = c0; it < c1; ++it)

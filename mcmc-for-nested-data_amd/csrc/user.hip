@@ -199,12 +199,12 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
         c.result = 0;
         return 0;
       }
-      c.result = (int64_t)x->d.RB * x->d.G <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
+      c.result = (int64_t)x->d.RB * x->d.G * x->d.S <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
       return 0;
     }
     case NMC_OP_CAPACITY: {
       int nb = 0;
-      if (int rc = user_fn(x, UK_RUN0 + NMC_MODE_NOPOOL, &f)) return rc;
+      if (int rc = user_fn(x, UK_RUN0 + run_mode(x), &f)) return rc;
       HIPCHK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f,
                                                                64 * x->d.W, run_lds_bytes(x)));
       c.result = nmc_safe_blocks(x, nb) * x->ncu;

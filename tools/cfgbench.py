@@ -1,0 +1,46 @@
+#!/usr/bin/env python
+"""Per-rank shard timings of the multi-GPU configs (diagnostics, not the contract
+bench): cfg 4 (1024 chains x 256 groups x 2000 obs over 8 GPUs -> 128 chains per rank,
+partial-pooling regression) and cfg 5 (512 x 128 x 5000 over 8 -> 64 chains per rank,
+8-parameter logistic, built-in family and the same model as a runtime-compiled user
+family)."""
+
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "mcmc-for-nested-data_amd"))
+
+from kbench import run  # noqa: E402
+
+LOGISTIC8 = r"""
+__device__ double nmc_user_loglik(const double* th, const double* row, const double* k) {
+  double eta = th[0];
+  for (int j = 0; j < 7; ++j) eta = fma(row[j], th[j + 1], eta);
+  double lae;
+  if (eta == 0.0) lae = NMC_LN2;
+  else lae = eta > 0.0 ? eta + log1p(exp(-eta)) : log1p(exp(eta));
+  return row[7] * eta - lae;
+}
+"""
+
+
+def main():
+    which = sys.argv[1:] or ["cfg4", "cfg5", "cfg5user"]
+    for w in which:
+        if w == "cfg4":
+            r = run("linreg", 128, 256, 2000, "partial", 0, 40)
+        elif w == "cfg5":
+            r = run("logistic", 64, 128, 5000, "partial", 0, 10)
+        else:
+            os.environ["KB_USER_SOURCE"] = LOGISTIC8
+            r = run("logistic", 64, 128, 5000, "partial", 0, 10)
+            os.environ.pop("KB_USER_SOURCE")
+        r["config"] = w
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

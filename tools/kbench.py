@@ -37,6 +37,10 @@ def engine_for(kind, C, G, N, pooling, waves, persist=None):
     elif kind == "logistic":
         X, y, _ = data.logistic(G, N, n_coef=8, seed=1)
         fam = Logistic(X, y)
+        if os.environ.get("KB_USER_SOURCE"):   # the same model as a user family (hiprtc)
+            from nestmc.families import DeviceLikelihood
+            fam = DeviceLikelihood(fam.obs(), os.environ["KB_USER_SOURCE"], fam.n_params,
+                                   host_function=fam)
         start = numpy.zeros(8)
     else:
         mu, sd = data.example_distribution(3, G)
