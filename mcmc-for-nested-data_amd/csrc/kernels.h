@@ -54,6 +54,7 @@ struct Dev {
   // its chain blocks RB = ceil(C / CL).  CB = ceil(C / 64) for every other kernel.
   int CL, RB;
   int paired;            // likelihood rows: two chains per lane (nmc_ll_rows_lds<Fam, true>)
+  int vzin;              // Philox step variates drawn in the step kernel (not by nmc_k_fill)
   // Row split (none/complete pooling with large groups): S workgroups ("members") share
   // one (chain block, group), member m owning the m-th contiguous chunk of the group's
   // rows (nmc_chunk); each step they exchange their partial sums through xbuf
@@ -1355,9 +1356,24 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   auto zl_src = [&](int tn, int pn) -> const double* {
     return d.vzl + ((size_t)(tn - d.vbase) * PGC + (size_t)pn * G * C + gc) * 2;
   };
+  // {z, log u} of step (tn, pn) -> LDS slot: Philox drawn here by the control wave
+  // (d.vzin: nmc_k_fill's formulas, no HBM round trip), or LDS-DMA of the replayed
+  // variates nmc_k_fill wrote
+  auto put_zl = [&](int tn, int pn, int slot) {
+    double* z = lds + (L.zl + 2 * slot) * 64;
+    if (d.vzin) {
+      const uint32_t ch = (uint32_t)(d.chain_base + cc);
+      const double zz = nmc_normal(tn, g, pn, NMC_PURPOSE_PROPOSAL, ch, d.seed);
+      const double lu = log(nmc_uniform2(tn, g, pn, NMC_PURPOSE_ACCEPT, ch, d.seed).a);
+      z[2 * lane] = zz;
+      z[2 * lane + 1] = lu;
+    } else {
+      nmc_dma16(zl_src(tn, pn), z);
+    }
+  };
   double* cwv = lds + L.cw * 64 + lane;    // cwv[k * 64]: control-wave values across barriers
   if (ctl) {     // {z, log u} of the first step -> LDS slot of step i0*P
-    nmc_dma16(zl_src(i0, 0), lds + (L.zl + 2 * ((i0 * P) & 1)) * 64);
+    put_zl(i0, 0, (i0 * P) & 1);
     for (int j = 0; j < Fam::NACC; ++j)   // x + (-0.0) == x: the fixed slot sum
       for (int k = nt; k < NMC_NSLOT; ++k) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = -0.0;
     nmc_drain_vm();
@@ -1674,7 +1690,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         }
         const int tn = p + 1 < P ? t : t + 1;
         const int pn = p + 1 < P ? p + 1 : 0;
-        if (tn < i1) nmc_dma16(zl_src(tn, pn), lds + (L.zl + 2 * (sp ^ 1)) * 64);
+        if (tn < i1) put_zl(tn, pn, sp ^ 1);
             };
       bool ctl_done = !ctl;
       if (ctl) {

@@ -97,6 +97,14 @@ static void choose_geometry(nmc_ctx* x) {
            (size_t)nmc_pair_lds(x->nacc, d.nmax * x->nf).total * 512 <= (size_t)160 * 1024 &&
            getenv("NMC_PAIR") && atoi(getenv("NMC_PAIR"));
   if (d.pair && d.W < 4) d.W = 4;
+  // Philox step variates drawn in the step kernel's control-wave slack instead of by
+  // nmc_k_fill (NMC_VZIN=1; Philox mode, not the pair kernel).  Measured on MI355X at
+  // cfg 3: 8.97 us/iter against 8.59 with the fill -- Box-Muller's fp64 log/sqrt/cos on
+  // the control wave's critical path costs more than the fill's 524 KB round trip -- so
+  // the fill stays the default.
+  d.vzin = 0;
+  if (const char* e = getenv("NMC_VZIN"))
+    d.vzin = x->rng == NMC_RNG_PHILOX && !d.pair && atoi(e) != 0;
   // likelihood rows in LDS for a family whose row blocks pair up (<= 4 fields): each lane
   // evaluates its rows for two chains (kernels.h nmc_ll_rows_lds<Fam, true>), half the LDS
   // reads; NMC_ROWS=bcast keeps the one-chain broadcast loop (same sums bit for bit)
@@ -535,10 +543,13 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       const int c1 = c0 + chunk < iter_end ? c0 + chunk : iter_end;
       // every variate of iterations [c0, c1) in one fully parallel launch
       x->d.vbase = c0;
-      const size_t n = (size_t)(c1 - c0) * P * x->C * (x->G + (partial ? 1 : 0));
-      const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);
-      hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);
-      HIPCHK(hipGetLastError());
+      const size_t n =
+          (size_t)(c1 - c0) * P * x->C * ((x->d.vzin ? 0 : x->G) + (partial ? 1 : 0));
+      if (n) {
+        const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);
+        hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);
+        HIPCHK(hipGetLastError());
+      }
       if (!partial) {
         if (x->d.S > 1)   // row split: fresh exchange counters for the launch
           HIPCHK(hipMemsetAsync(x->d.xcnt, 0, (size_t)x->d.RB * x->d.G * 32 * sizeof(unsigned),

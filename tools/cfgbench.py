@@ -32,6 +32,8 @@ def main():
     for w in which:
         if w == "cfg4":
             r = run("linreg", 128, 256, 2000, "partial", 0, 40)
+        elif w == "cfg4w4":   # four waves per workgroup: two workgroups per CU, resident
+            r = run("linreg", 128, 256, 2000, "partial", 4, 40)
         elif w == "cfg5":
             r = run("logistic", 64, 128, 5000, "partial", 0, 10)
         else:
