@@ -48,13 +48,14 @@
 
 struct Dev {
   int C, G, P, pooling, nf, chain_base, rng_mode, W, CB;
-  // step kernel: chains per workgroup (64: one chain per lane; 32: the half-lane layout,
-  // lanes l and l + 32 hold the same chain and split every row pair of the likelihood,
-  // so two workgroups share a CU where one 64-chain workgroup would hold it alone) and
-  // its chain blocks RB = ceil(C / CL).  CB = ceil(C / 64) for every other kernel.
+  // step kernel: chains per workgroup CL (64, one per lane; reported by
+  // nmc_launch_config) and its chain blocks RB = ceil(C / CL).  (A 32-chain half-lane
+  // layout -- two workgroups per CU -- measured 11.5 against 8.5 us per iteration at
+  // cfg 3 and was removed.)
   int CL, RB;
   int paired;            // likelihood rows: two chains per lane (nmc_ll_rows_lds<Fam, true>)
   int vzin;              // Philox step variates drawn in the step kernel (not by nmc_k_fill)
+  int gtiles;            // register Gibbs mode: the Gibbs wave takes likelihood tiles too
   // Row split (none/complete pooling with large groups): S workgroups ("members") share
   // one (chain block, group), member m owning the m-th contiguous chunk of the group's
   // rows (nmc_chunk); each step they exchange their partial sums through xbuf
@@ -162,14 +163,12 @@ struct Dev {
 #define NMC_STAMP_AT(k, slot) do {} while (0)
 #endif
 
-// The chain of this lane in step-kernel chain block cb, and whether the lane owns its
-// outputs (half-lane layout: lanes 32-63 mirror lanes 0-31 and store nothing).
-__device__ __forceinline__ int nmc_lane_chain(const Dev& d, int cb, int lane) {
-  return cb * d.CL + (lane & (d.CL - 1));
+// The chain of this lane in step-kernel chain block cb (64 chains per workgroup, one per
+// lane), and whether the lane's chain exists.
+__device__ __forceinline__ int nmc_lane_chain(const Dev&, int cb, int lane) {
+  return cb * 64 + lane;
 }
-__device__ __forceinline__ bool nmc_lane_owns(const Dev& d, int c, int lane) {
-  return c < d.C && lane < d.CL;
-}
+__device__ __forceinline__ bool nmc_lane_owns(const Dev& d, int c, int) { return c < d.C; }
 
 // Both halves' values of v in every lane (v_permlane32_swap, gfx950): lo = lanes 0-31's
 // value of the lane's pair, hi = lanes 32-63's.
@@ -1517,7 +1516,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             }
           }
         }
-        lik_tiles(t, p, gs & 1, []() {});
+        if (d.gtiles) lik_tiles(t, p, gs & 1, []() {});
         __syncthreads();   // A
         if (due) {
           ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
@@ -1585,7 +1584,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             // keep the payload loads below the poll (no instruction: wavefront scope)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const double* src = (atq & 1) ? d.vb1 : d.vb0;
-            if ((C & 1) == 0 && d.CL == 64) {
+            if ((C & 1) == 0) {
               nmc_hyper_dma(d, src, aq, cb, 0, G, lds, L, 0);
               nmc_drain_vm();
             } else {
@@ -1639,7 +1638,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             // keep the payload loads below the poll (no instruction: wavefront scope)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const double* src = (atq & 1) ? d.vb1 : d.vb0;
-            if ((C & 1) == 0 && d.CL == 64)
+            if ((C & 1) == 0)
               nmc_hyper_dma(d, src, aq, cb, 0, G, lds, L, ((gs - 1) & 1) * (G + 1));
             else
               nmc_hyper_load(d, src, aq, cc, 0, G, lds, L, ((gs - 1) & 1) * (G + 1));
@@ -1831,7 +1830,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     if (!hr && pub && gw) {
       const double* src = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
       const int ho = ((ge - 1) & 1) * (G + 1);
-      if ((C & 1) == 0 && d.CL == 64) {
+      if ((C & 1) == 0) {
         nmc_hyper_dma(d, src, P - 1, cb, 0, G, lds, L, ho);
         nmc_drain_vm();
       } else {

@@ -103,6 +103,8 @@ static void choose_geometry(nmc_ctx* x) {
   // the control wave's critical path costs more than the fill's 524 KB round trip -- so
   // the fill stays the default.
   d.vzin = 0;
+  d.gtiles = 0;   // (NMC_GIBBS_TILES=1: measured no better at cfg 3)
+  if (const char* e = getenv("NMC_GIBBS_TILES")) d.gtiles = atoi(e) != 0;
   if (const char* e = getenv("NMC_VZIN"))
     d.vzin = x->rng == NMC_RNG_PHILOX && !d.pair && atoi(e) != 0;
   // likelihood rows in LDS for a family whose row blocks pair up (<= 4 fields): each lane
