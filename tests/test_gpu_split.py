@@ -68,3 +68,27 @@ def test_split_shard_and_batch_invariance(gpu_lib):
     assert single[3]["split_members"] == 1
     assert numpy.array_equal(single[0], whole[0])
     assert close(single[1], whole[1], rtol=1e-12) and close(single[2], whole[2], rtol=1e-12)
+
+
+def test_split_ragged_and_empty_groups(gpu_lib):
+    """Members whose chunk of a small group is empty, and an empty group, under the split
+    (S fixed by the largest group): against the oracle."""
+    import scipy.stats
+    from nestmc.families import LinearRegression
+    r = numpy.random.RandomState(8)
+    sizes = [30000, 5, 0, 17000]
+    n = sum(sizes)
+    x = r.normal(size=n)
+    y = 1.0 + 3.0 * x + r.normal(size=n) * 0.7
+    fam = LinearRegression(numpy.vstack([numpy.ones(n), x]).T, y)
+    priors = [scipy.stats.norm(0, 10), scipy.stats.norm(3, 10), scipy.stats.gamma(2)]
+    C, P = 66, 3
+    st, nested = _synthetic_state(fam, sizes, priors, "none", C, P, len(sizes))
+    acc, llp, rows, cfg = run_engine(fam, sizes, st, numpy.arange(C), 0, 12, 21, pooling="none",
+                                     priors=priors, tune_interval=5)
+    assert cfg["split_members"] > 5, cfg
+    oacc, ollp, orows, margin = run_oracle(nested, st, numpy.arange(3), numpy.arange(3), 12, 21,
+                                           pooling="none", priors=priors, tune_interval=5)
+    assert numpy.array_equal(acc[:3].astype(bool), oacc), margin
+    assert close(llp[:3], ollp, rtol=1e-10)
+    assert close(rows[:3], orows)
