@@ -235,7 +235,7 @@ struct nmc_lds_layout {
   int hleaf;   // [P][nleaf]     leaf sums
   int zl;      // [2][2]         {z, log u} of this and the next step (LDS-DMA, step parity)
   int hv;      // [2P]           {hyper z, gamma} of the Gibbs update (LDS-DMA)
-  int cw;      // [16]           control-wave values across the step barriers
+  int cw;      // [8]            control-wave values across the step barriers
   int flag;    // [1]            broadcast / epoch words
   int xchg;    // [2][8]         stream sums exchanged by the two compute waves
   int rows;    // [nrows_lds][NF] the group's observation rows (staged once per launch)
@@ -255,7 +255,7 @@ __host__ __device__ inline nmc_lds_layout nmc_lds(int nacc, int P, int partial, 
   L.zl = L.hleaf + (partial ? P * nleaf : 0);
   L.hv = L.zl + 4;
   L.cw = L.hv + (partial ? 2 * P : 0);
-  L.flag = L.cw + 16;
+  L.flag = L.cw + 8;    // (NMC_CW_* uses 7 columns)
   L.xchg = L.flag + 1;
   L.rows = L.xchg;
   // (+1 column: the pipelined likelihood loop prefetches one block past a wave's rows)
@@ -305,6 +305,9 @@ __device__ __forceinline__ void nmc_drain_vm() { asm volatile("s_waitcnt vmcnt(0
 //     draw} of iteration t, [p][lane][2].
 // Out: LDS hyp mu/sd/lsd/s2; write: global mu/s2/sd/lsd + the sample row of t.
 // ---------------------------------------------------------------------------
+#ifndef NMC_HYPER_NS
+#define NMC_HYPER_NS 1   // streams per wave-iteration (2 and 4 measured slower at cfg 4)
+#endif
 template <int SRC, bool SQ>
 __device__ __forceinline__ void nmc_hyper_streams(const Dev& d, const double* src, int cc,
                                                   double* lds, const nmc_lds_layout& L) {
@@ -314,43 +317,69 @@ __device__ __forceinline__ void nmc_hyper_streams(const Dev& d, const double* sr
   const int P = d.P, G = d.G, C = d.C, nl = d.nleaf, ncol = 8 + d.ntail;
   const int per = 8 + (d.ntail ? 1 : 0);
   const int nst = P * nl * per;
-  for (int s = w; s < nst; s += W) {
-    const int j = s % per, pl = s / per;    // pl = p * nleaf + leaf
-    const int lf = pl % nl, p = pl / nl;
-    const int a = nl == 1 ? 0 : d.leaf[lf], m = nl == 1 ? G : d.leaf[lf + 1] - a;
-    const int m8 = m >= 8 ? m - m % 8 : 0;
+  // NS streams per wave-iteration, their loads in flight together
+  constexpr int NS = NMC_HYPER_NS;
+  struct Strm {
+    int j, pl, p, m, m8;
+    const double* xp;
+  };
+  auto strm = [&](int s) {
+    Strm q;
+    q.j = s % per;
+    q.pl = s / per;   // pl = p * nleaf + leaf
+    const int lf = q.pl % nl;
+    q.p = q.pl / nl;
+    const int a = nl == 1 ? 0 : d.leaf[lf];
+    q.m = nl == 1 ? G : d.leaf[lf + 1] - a;
+    q.m8 = q.m >= 8 ? q.m - q.m % 8 : 0;
     // element k of the leaf for this lane's chain
-    const double* xp = SRC == NMC_SRC_LDS ? lds + (size_t)(L.hval + p * G + a) * 64 + lane
-                                          : src + ((size_t)p * G + a) * C + cc;
-    const size_t xs = SRC == NMC_SRC_LDS ? 64 : (size_t)C;
-    double* out = lds + (size_t)(L.hst + pl * ncol) * 64 + lane;
-    const double mu = SQ ? lds[(L.hyp + NMC_HY_MU * P + p) * 64 + lane] : 0.0;
-    if (j < 8) {
-      const int cnt = m8 >> 3;   // <= 16
-      double t[16];
+    q.xp = SRC == NMC_SRC_LDS ? lds + (size_t)(L.hval + q.p * G + a) * 64 + lane
+                              : src + ((size_t)q.p * G + a) * C + cc;
+    return q;
+  };
+  const size_t xs = SRC == NMC_SRC_LDS ? 64 : (size_t)C;
+  for (int s0 = w; s0 < nst; s0 += W * NS) {
+    double t[NS][16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) t[u] = u < cnt ? nmc_ldv<SRC>(xp + (size_t)(j + 8 * u) * xs) : 0.0;
-      double r = 0.0;
+    for (int k = 0; k < NS; ++k) {
+      const int s = s0 + k * W;
+      const Strm q = strm(s < nst ? s : s0);
+      const int cnt = s < nst && q.j < 8 ? q.m8 >> 3 : 0;   // <= 16
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        if (u < cnt) {
-          double v = t[u];
+      for (int u = 0; u < 16; ++u)
+        t[k][u] = u < cnt ? nmc_ldv<SRC>(q.xp + (size_t)(q.j + 8 * u) * xs) : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const int s = s0 + k * W;
+      if (s >= nst) continue;
+      const Strm q = strm(s);
+      double* out = lds + (size_t)(L.hst + q.pl * ncol) * 64 + lane;
+      const double mu = SQ ? lds[(L.hyp + NMC_HY_MU * P + q.p) * 64 + lane] : 0.0;
+      if (q.j < 8) {
+        const int cnt = q.m8 >> 3;
+        double r = 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          if (u < cnt) {
+            double v = t[k][u];
+            if (SQ) {
+              v = v - mu;
+              v = v * v;
+            }
+            r = u == 0 ? v : r + v;
+          }
+        }
+        out[q.j * 64] = r;
+      } else {
+        for (int u = q.m8; u < q.m; ++u) {
+          double v = nmc_ldv<SRC>(q.xp + (size_t)u * xs);
           if (SQ) {
             v = v - mu;
             v = v * v;
           }
-          r = u == 0 ? v : r + v;
+          out[(8 + u - q.m8) * 64] = v;
         }
-      }
-      out[j * 64] = r;
-    } else {
-      for (int u = m8; u < m; ++u) {
-        double v = nmc_ldv<SRC>(xp + (size_t)u * xs);
-        if (SQ) {
-          v = v - mu;
-          v = v * v;
-        }
-        out[(8 + u - m8) * 64] = v;
       }
     }
   }

@@ -107,6 +107,19 @@ static void choose_geometry(nmc_ctx* x) {
   if (const char* e = getenv("NMC_GIBBS_TILES")) d.gtiles = atoi(e) != 0;
   if (const char* e = getenv("NMC_VZIN"))
     d.vzin = x->rng == NMC_RNG_PHILOX && !d.pair && atoi(e) != 0;
+  // Partial pooling whose grid is more than one 8-wave workgroup per CU but fits two
+  // 4-wave ones (cfg-4 shards: 2 chain blocks x 256 groups): four waves, so the whole
+  // grid is resident and runs persistent (both chain blocks' workgroups share each CU
+  // and interleave their serial phases) -- measured 48.5 against 67.6 us/iter in
+  // launch-per-iteration mode at 128 x 256 x 2000.
+  if (x->pooling == NMC_POOL_PARTIAL && d.W > 4 && !getenv("NMC_WAVES")) {
+    const int64_t wgs = (int64_t)d.RB * d.G * d.S;
+    if (wgs > x->ncu && wgs <= 2 * (int64_t)x->ncu) {
+      const int w8 = d.W;
+      d.W = 4;
+      if (lds_bytes_for(x, d.hlds, d.rows_lds) > (size_t)80 * 1024) d.W = w8;
+    }
+  }
   // likelihood rows in LDS for a family whose row blocks pair up (<= 4 fields): each lane
   // evaluates its rows for two chains (kernels.h nmc_ll_rows_lds<Fam, true>), half the LDS
   // reads; NMC_ROWS=bcast keeps the one-chain broadcast loop (same sums bit for bit)
