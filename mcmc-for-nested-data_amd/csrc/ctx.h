@@ -78,8 +78,8 @@ static inline int run_mode(const nmc_ctx* x) {
   if (x->pooling != NMC_POOL_PARTIAL) return NMC_MODE_NOPOOL;
   if (!x->persistent) return NMC_MODE_LAUNCH;
   if (x->d.pair) return NMC_MODE_PAIR;
-  if (!x->d.hlds) return NMC_MODE_SYNC;
-  return x->d.hreg ? NMC_MODE_SYNC_REG : NMC_MODE_SYNC_LDS;
+  if (x->d.hreg) return NMC_MODE_SYNC_REG;
+  return x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
 }
 
 static inline size_t run_lds_bytes(const nmc_ctx* x) {
@@ -99,7 +99,7 @@ static inline int nmc_safe_blocks(const nmc_ctx* x, int nb) {
 static inline size_t pair_lds_bytes(const nmc_ctx* x);
 // LDS of the persistent partial-pooling kernel (its occupancy query)
 static inline size_t nmc_persist_lds(const nmc_ctx* x) {
-  return x->d.pair ? pair_lds_bytes(x) : lds_bytes_for(x, x->d.hlds, x->d.rows_lds);
+  return x->d.pair ? pair_lds_bytes(x) : lds_bytes_for(x, x->d.hlds && !x->d.hreg, x->d.rows_lds);
 }
 
 static inline int pop_event_pair(nmc_ctx* x, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v,

@@ -44,9 +44,9 @@ static bool nmc_can_persist(nmc_ctx* x) {
   if (const char* e = getenv("NMC_PERSIST")) return atoi(e) != 0;
   int nb = 0;
   const void* k = x->d.pair   ? (const void*)nmc_k_pair<Fam>
-                  : !x->d.hlds ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC>
                   : x->d.hreg  ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_REG>
-                               : (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_LDS>;
+                  : x->d.hlds  ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_LDS>
+                               : (const void*)nmc_k_run<Fam, NMC_MODE_SYNC>;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W, nmc_persist_lds(x)) !=
       hipSuccess)
     return false;

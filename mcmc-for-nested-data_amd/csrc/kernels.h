@@ -1153,6 +1153,10 @@ __device__ __forceinline__ double nmc_pairwise_reg(const double (&x)[64], int G,
   return res;
 }
 
+__device__ __forceinline__ void nmc_hyper_finish(const Dev& d, int cb, int t, int p, double* lds,
+                                                 int hyp, bool write, double mu, double ss,
+                                                 double hx);
+
 // The Gibbs update of parameter p after iteration t for this wave's 64 chains from the
 // chain block's values x[0..G) of p in registers (G <= 64); otherwise identical to
 // nmc_hyper_compute (same sums in the same order, same draws, same outputs).
@@ -1169,6 +1173,18 @@ __device__ __forceinline__ void nmc_hyper_compute_reg(const Dev& d, int cb, int 
   const double tot = nmc_pairwise_reg(x, G, false, 0.0);
   const double mu = tot / G + sdm * hz;                        // mu ~ N(mean(x), sqrt(s2/G))
   const double ss = nmc_pairwise_reg(x, G, true, mu);
+  nmc_hyper_finish(d, cb, t, p, lds, hyp, write, mu, ss, hx);
+}
+
+// mu and sum((x - mu)^2) -> sigma2 draw, LDS hyper state, (write) global slot of t and
+// the sample row of t (HyperParameter._updateVar :489-498, setPrior :273-282).
+__device__ __forceinline__ void nmc_hyper_finish(const Dev& d, int cb, int t, int p, double* lds,
+                                                 int hyp, bool write, double mu, double ss,
+                                                 double hx) {
+  const int lane = threadIdx.x & 63;
+  const int P = d.P, G = d.G, C = d.C;
+  const int c = nmc_lane_chain(d, cb, lane);
+  double* hy = lds + hyp * 64 + lane;
   const double hat = ss / (double)(G - 1);
   const double scale = d.ha * hat;
   // scipy invgamma.rvs: (1/gammainccinv(a, U)) * scale + loc; loc when scale == 0
@@ -1265,6 +1281,78 @@ __device__ __forceinline__ void nmc_split_exchange(const Dev& d, int cb, int g, 
     acc[j] = S >= 4 ? (s4[0] + s4[1]) + (s4[2] + s4[3])
                     : (S == 1 ? s4[0] : (S == 2 ? s4[0] + s4[1] : (s4[0] + s4[1]) + s4[2]));
   }
+}
+
+// numpy's pairwise sum over the chain block's G (64 < G <= 256) values of one parameter,
+// streamed from global memory (sc1) in chunks of 64: each numpy leaf (<= 128 values, the
+// host plan d.leaf) as 8 interleaved streams carried across chunks plus its tail in
+// order, the leaves merged in numpy's recursion order (d.merge) -- the order of
+// nmc_hyper_compute and the oracle.  src: the parameter's [G][C] values + this chain.
+__device__ __forceinline__ double nmc_pairwise_stream(const Dev& d, const double* src, bool sq,
+                                                      double mu) {
+  const int C = d.C, G = d.G, nl = d.nleaf;
+  auto tr = [&](double v) {
+    if (sq) {
+      v = v - mu;
+      v = v * v;
+    }
+    return v;
+  };
+  double ls[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int lf = 0; lf < nl; ++lf) {
+    const int a = nl == 1 ? 0 : d.leaf[lf];
+    const int m = nl == 1 ? G : d.leaf[lf + 1] - a;
+    const int m8 = m >= 8 ? m - m % 8 : 0;
+    double r[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int e0 = 0; e0 < m8; e0 += 64) {
+      double x[64];
+#pragma unroll
+      for (int k = 0; k < 64; ++k)
+        x[k] = e0 + k < m8 ? nmc_ldv<NMC_SRC_SC1>(src + (size_t)(a + e0 + k) * C) : 0.0;
+#pragma unroll
+      for (int k = 0; k < 64; ++k)
+        if (e0 + k < m8) r[k & 7] = e0 + k < 8 ? tr(x[k]) : r[k & 7] + tr(x[k]);
+    }
+    double res = m8 ? ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7])) : 0.0;
+    for (int e = m8; e < m; ++e) res += tr(nmc_ldv<NMC_SRC_SC1>(src + (size_t)(a + e) * C));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i == lf) ls[i] = res;
+  }
+  for (int k = 0; k < d.nmerge; ++k) {   // slot A += slot B
+    const int A = d.merge[2 * k], B = d.merge[2 * k + 1];
+    double vb = ls[0];
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+      if (i == B) vb = ls[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i == A) ls[i] = ls[i] + vb;
+  }
+  return ls[0];
+}
+
+// The register Gibbs update of task (tq, q) for this wave's 64 chains: G <= 64 from one
+// 64-value fetch (nmc_hyper_fetch_reg / _compute_reg), 64 < G <= 256 streamed
+// (nmc_pairwise_stream, two passes).  Same sums, draws and outputs either way.
+__device__ __forceinline__ void nmc_hyper_update_reg(const Dev& d, int cb, int tq, int q, int cc,
+                                                     double* lds, int hyp, bool write) {
+  if (d.G <= 64) {
+    double xv[64], fz, fx;
+    nmc_hyper_fetch_reg(d, tq, q, cc, xv, fz, fx);
+    nmc_hyper_compute_reg(d, cb, tq, q, lds, hyp, write, fz, fx, xv);
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const int P = d.P, G = d.G, C = d.C;
+  const double* src = ((tq & 1) ? d.vb1 : d.vb0) + (size_t)q * G * C + cc;
+  const size_t hvi = (((size_t)(tq - d.vbase) * P + q) * C + cc) * 2;
+  const double hz = d.vh[hvi], hx = d.vh[hvi + 1];
+  const double sdm = sqrt(lds[(hyp + NMC_HY_S2 * P + q) * 64 + lane] / G);
+  const double tot = nmc_pairwise_stream(d, src, false, 0.0);
+  const double mu = tot / G + sdm * hz;                        // mu ~ N(mean(x), sqrt(s2/G))
+  const double ss = nmc_pairwise_stream(d, src, true, mu);
+  nmc_hyper_finish(d, cb, tq, q, lds, hyp, write, mu, ss, hx);
 }
 
 // ---------------------------------------------------------------------------
@@ -1524,13 +1612,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
           if (r) {
             // keep the payload loads below the poll (no instruction: wavefront scope)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            double xv[64], fz, fx;
-            nmc_hyper_fetch_reg(d, kt, kq, cc, xv, fz, fx);
-#ifdef NMC_STAMPS
-            nmc_drain_vm();
-            if (p == 0) NMC_STAMP_AUX(t, 14);
-#endif
-            nmc_hyper_compute_reg(d, cb, kt, kq, lds, L.hyp, g0w, fz, fx, xv);
+            nmc_hyper_update_reg(d, cb, kt, kq, cc, lds, L.hyp, g0w);
             if (p == 0) NMC_STAMP_AUX(t, 15);
             if (P <= 2) {   // the update lands in the step that needs it: this step's priors
               const int sp = gs & 1;
@@ -1560,9 +1642,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       const int ge = i1 * P;
       if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L)) {
         for (int k = ge - lag > gs0 ? ge - lag : gs0; k < ge; ++k) {
-          double xv[64], fz, fx;
-          nmc_hyper_fetch_reg(d, k / P, k % P, cc, xv, fz, fx);
-          nmc_hyper_compute_reg(d, cb, k / P, k % P, lds, L.hyp, true, fz, fx, xv);
+          nmc_hyper_update_reg(d, cb, k / P, k % P, cc, lds, L.hyp, true);
         }
       }
     }

@@ -74,7 +74,7 @@ static void choose_geometry(nmc_ctx* x) {
     if (v >= 16 && v % 16 == 0) d.tile = v;
   }
   // partial pooling, persistent payload-in-LDS mode: wave 1 is the Gibbs wave
-  d.naux = x->pooling == NMC_POOL_PARTIAL && d.W >= 3 && d.G <= 128 ? 1 : 0;
+  d.naux = x->pooling == NMC_POOL_PARTIAL && d.W >= 3 && d.G <= 256 ? 1 : 0;
   // rows in LDS when they fit beside the rest of the carve (64 KiB for the rows)
   d.rows_lds = (size_t)d.nmax * x->nf * 8 <= (size_t)64 * 1024 &&
                lds_bytes_for(x, 0, 1) <= (size_t)96 * 1024 &&
@@ -87,7 +87,13 @@ static void choose_geometry(nmc_ctx* x) {
            !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
   // G <= 64: the Gibbs wave fetches a task's values into registers (one sc1 round trip)
   // and updates in the step after publication (no LDS payload, no two-stage pipeline)
-  d.hreg = d.hlds && d.G <= 64 && !(getenv("NMC_NO_HREG") && atoi(getenv("NMC_NO_HREG")));
+  // (NMC_HREG_STREAM=1, 64 < G <= 256: the values streamed through registers in 64-value
+  // chunks, two passes, nmc_pairwise_stream; measured 61 against 53 us/iter for the
+  // all-wave update at the cfg-4 shard -- one wave's four serial round trips per pass
+  // land on the step that needs the priors -- so opt-in)
+  const bool stream = getenv("NMC_HREG_STREAM") && atoi(getenv("NMC_HREG_STREAM"));
+  d.hreg = d.naux > 0 && (d.G <= 64 ? d.hlds : stream && d.nleaf <= 4) &&
+           !(getenv("NMC_NO_HREG") && atoi(getenv("NMC_NO_HREG")));
   // P == 2 with rows in LDS: both steps of an iteration from one pass (pair.h); needs
   // the control wave, two Gibbs waves and at least one likelihood wave
   // (measured on MI355X at cfg 3: 8.6-9.8 us per iteration against 8.0 for SYNC_REG --

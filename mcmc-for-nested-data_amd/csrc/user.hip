@@ -190,8 +190,8 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
         c.result = atoi(e) != 0;
         return 0;
       }
-      const int mode = !x->d.hlds ? NMC_MODE_SYNC : x->d.hreg ? NMC_MODE_SYNC_REG
-                                                               : NMC_MODE_SYNC_LDS;
+      const int mode = x->d.hreg ? NMC_MODE_SYNC_REG
+                                 : x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
       int nb = 0;
       if (int rc = user_fn(x, UK_RUN0 + mode, &f)) return rc;
       if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * x->d.W,

@@ -49,14 +49,20 @@ def test_cfg4_geometry_multileaf_gibbs(gpu_lib, G):
     # one chain block: G workgroups, co-resident -> persistent (SYNC, multi-leaf plan)
     one = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed)
     assert one[3]["persistent"], one[3]
-    # the same chains in a two-block launch (launch per iteration at G = 256) and forced
-    # launch per iteration
+    # the same chains in a two-block launch (two 4-wave workgroups per CU, persistent) and
+    # forced launch per iteration
     two = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed)
     lau = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, env={"NMC_PERSIST": "0"})
     assert not lau[3]["persistent"]
+    # the register hand-off with the values streamed in 64-value chunks (opt-in)
+    reg = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed,
+                     env={"NMC_HREG_STREAM": "1"})
+    if G == 256:   # (G = 129: 258 workgroups of > 80 KB LDS -> launch per iteration)
+        assert reg[3]["mode"] == "NMC_MODE_SYNC_REG", reg[3]
     for k in range(3):
         assert numpy.array_equal(one[k], two[k][:64], equal_nan=True), k
         assert numpy.array_equal(two[k], lau[k], equal_nan=True), k
+        assert numpy.array_equal(two[k], reg[k], equal_nan=True), k
     assert 0.05 < lau[0].mean() < 0.95
     # chains 0, 1 and 127 against the oracle
     sel = numpy.array([0, 1, 127])
