@@ -107,3 +107,28 @@ def test_gpu_variogram_matches_reference_sums(gpu_lib):
     for k in (0, 7, 23):
         want = numpy.array([od.variogram(x[k], t) for t in range(300)])
         assert numpy.allclose(got[k], want, rtol=1e-12, atol=0)
+
+
+@pytest.mark.gpu
+def test_gpu_sample_then_diagnose(gpu_lib, tmp_path):
+    """The drop-in pair end to end: samplePosterior (GPU) writes the sample files,
+    diagnoseSamples (GPU variogram) reads them; its files equal the oracle
+    restatement's on the same files."""
+    import posteriorSampling
+    import sampleDiagnosis
+    from gpu_cases import synthetic
+    fam, sizes, _, _, _ = synthetic("linreg_partial", 4, 5, 40)
+    out = str(tmp_path / "run")
+    posteriorSampling.samplePosterior(4, 400, 200, ("b0", "b1"), 5, 40, "partial", fam, out,
+                                      saveLogLikelihood=False,
+                                      startingPointValueRange={"b0": [-1, 1], "b1": [0, 3]},
+                                      displayProgress=False)
+    with contextlib.redirect_stdout(io.StringIO()):
+        sampleDiagnosis.diagnoseSamples(out, nFigures=0)
+    src = os.path.join(out, "sample")
+    a, partial, complete = od.assess(src)
+    got = open(os.path.join(out, "diagnostic", "diagnosticAssessment.csv")).read()
+    assert got == od.assessment_text(a, False)
+    assert open(os.path.join(out, "diagnostic", "diagnosticAssessmentIndividual.csv")).read() \
+        == od.individual_text(a)
+    assert open(os.path.join(src, "summary.csv")).read() == od.summary_text(src)
