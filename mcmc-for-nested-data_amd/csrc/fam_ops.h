@@ -5,35 +5,31 @@
 
 // Iterations [i0, i1) of the step kernel (one launch, or one per resident chain-block
 // batch under the row split).
+// The step kernel instance of (mode, rows in LDS) -- for launches and occupancy queries.
+template <class Fam, bool RL>
+static const void* nmc_run_kernel_rl(int mode) {
+  switch (mode) {
+    case NMC_MODE_NOPOOL: return (const void*)nmc_k_run<Fam, NMC_MODE_NOPOOL, RL>;
+    case NMC_MODE_LAUNCH: return (const void*)nmc_k_run<Fam, NMC_MODE_LAUNCH, RL>;
+    case NMC_MODE_SYNC: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC, RL>;
+    case NMC_MODE_SYNC_REG: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_REG, RL>;
+    case NMC_MODE_PAIR: return (const void*)nmc_k_pair<Fam>;
+    default: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_LDS, RL>;
+  }
+}
+template <class Fam>
+static const void* nmc_run_kernel(const nmc_ctx* x, int mode) {
+  return x->d.rows_lds ? nmc_run_kernel_rl<Fam, true>(mode) : nmc_run_kernel_rl<Fam, false>(mode);
+}
+
 template <class Fam>
 static int nmc_launch_run(nmc_ctx* x, const Fam& fam, int i0, int i1, int flags) {
   return nmc_run_launches(x, i0, i1, [&](int mode, const Dev& d, dim3 grid, dim3 block,
                                          size_t lds) {
-    switch (mode) {
-      case NMC_MODE_NOPOOL:
-        hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_NOPOOL>), grid, block, lds, x->stream, d, fam,
-                           d.obs, i0, i1, flags);
-        break;
-      case NMC_MODE_LAUNCH:
-        hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_LAUNCH>), grid, block, lds, x->stream, d, fam,
-                           d.obs, i0, i1, flags);
-        break;
-      case NMC_MODE_SYNC:
-        hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC>), grid, block, lds, x->stream, d, fam,
-                           d.obs, i0, i1, flags);
-        break;
-      case NMC_MODE_PAIR:
-        hipLaunchKernelGGL((nmc_k_pair<Fam>), grid, block, lds, x->stream, d, fam, d.obs, i0, i1,
-                           flags);
-        break;
-      case NMC_MODE_SYNC_REG:
-        hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC_REG>), grid, block, lds, x->stream, d,
-                           fam, d.obs, i0, i1, flags);
-        break;
-      default:
-        hipLaunchKernelGGL((nmc_k_run<Fam, NMC_MODE_SYNC_LDS>), grid, block, lds, x->stream, d,
-                           fam, d.obs, i0, i1, flags);
-    }
+    Dev dd = d;
+    const double* obs = d.obs;
+    void* args[] = {&dd, (void*)&fam, (void*)&obs, &i0, &i1, &flags};
+    hipLaunchKernel(nmc_run_kernel<Fam>(x, mode), grid, block, args, lds, x->stream);
   });
 }
 
@@ -43,10 +39,10 @@ template <class Fam>
 static bool nmc_can_persist(nmc_ctx* x) {
   if (const char* e = getenv("NMC_PERSIST")) return atoi(e) != 0;
   int nb = 0;
-  const void* k = x->d.pair   ? (const void*)nmc_k_pair<Fam>
-                  : x->d.hreg  ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_REG>
-                  : x->d.hlds  ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_LDS>
-                               : (const void*)nmc_k_run<Fam, NMC_MODE_SYNC>;
+  const void* k = nmc_run_kernel<Fam>(x, x->d.pair   ? NMC_MODE_PAIR
+                                         : x->d.hreg ? NMC_MODE_SYNC_REG
+                                         : x->d.hlds ? NMC_MODE_SYNC_LDS
+                                                     : NMC_MODE_SYNC);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W, nmc_persist_lds(x)) !=
       hipSuccess)
     return false;
@@ -63,12 +59,7 @@ static int nmc_fam_call(nmc_ctx* x, const Fam& fam, NmcCall& c) {
       return 0;
     case NMC_OP_CAPACITY: {   // resident step-kernel workgroups of the run mode (safe count)
       int nb = 0;
-      const int mode = run_mode(x);
-      const void* k = mode == NMC_MODE_NOPOOL   ? (const void*)nmc_k_run<Fam, NMC_MODE_NOPOOL>
-                      : mode == NMC_MODE_SYNC   ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC>
-                      : mode == NMC_MODE_SYNC_REG ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_REG>
-                      : mode == NMC_MODE_SYNC_LDS ? (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_LDS>
-                                                  : (const void*)nmc_k_run<Fam, NMC_MODE_LAUNCH>;
+      const void* k = nmc_run_kernel<Fam>(x, run_mode(x));
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W, run_lds_bytes(x)) !=
           hipSuccess)
         return nmc_fail(-2, "occupancy query failed");

@@ -1386,7 +1386,10 @@ enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
                                  // values straight into registers and updates in one step
        NMC_MODE_PAIR = 5 };      // persistent, G <= 64, P == 2: both steps of an iteration
                                  // from one pass over the rows (pair.h, nmc_k_pair)
-template <class Fam, int MODE>
+// RL: the groups' rows are staged in LDS for the launch (d.rows_lds) -- a template
+// parameter so each instance holds only its own row loop (the LDS-DMA staged loop's
+// registers raised the rows-in-LDS kernel's pressure: ~5 % of its time at cfg 3)
+template <class Fam, int MODE, bool RL = true>
 __global__ void __launch_bounds__(512)
 nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int flags) {
   constexpr bool PARTIAL = MODE != NMC_MODE_NOPOOL;
@@ -1415,7 +1418,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const int lag = hr && P >= 2 ? 2 : 1;
   // rows in LDS for the launch, or every wave's two staging buffers (nmc_ll_rows_staged)
   const int row_doubles =
-      d.rows_lds ? d.nmax * Fam::NFIELDS : nmc_stage_doubles(Fam::NFIELDS, blockDim.x >> 6);
+      RL ? d.nmax * Fam::NFIELDS : nmc_stage_doubles(Fam::NFIELDS, blockDim.x >> 6);
   const nmc_lds_layout L =
       nmc_lds(Fam::NACC, P, PARTIAL, d.nleaf, d.ntail, W, G, hl && !hr ? 1 : 0, row_doubles);
   double* th = lds + L.th * 64 + lane;            // th[p * 64]: this lane's chain, parameter p
@@ -1465,7 +1468,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   }
   const double gcst = fam.gconst((long)ngrp);   // per-group constant of finish_fast
   double* lrows = lds + L.rows * 64;
-  if (d.rows_lds) {   // this group's rows -> LDS, once for the whole launch
+  if constexpr (RL) {   // this group's rows -> LDS, once for the whole launch
     const int nd = nrow * Fam::NFIELDS;
     for (int i = threadIdx.x; i < nd; i += blockDim.x) lrows[i] = grows[i];
   }
@@ -1573,15 +1576,16 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       const int rn = TI.len(k);
       NMC_TILE_STAMP(k, 0);
       double acc[Fam::NACC];
-      bool done = false;
-      if constexpr (nmc_paired_rows_ok<Fam>()) if (d.rows_lds && d.paired) {
-        // two chains per lane, row pairs split by lane half
-        nmc_ll_rows_lds<Fam, true>(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc, &preg);
-        done = true;
-      }
-      if (done) {
-      } else if (d.rows_lds) {   // wave-uniform LDS address: broadcast ds_reads, pipelined
-        nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
+      if constexpr (RL) {
+        bool done = false;
+        if constexpr (nmc_paired_rows_ok<Fam>()) if (d.paired) {
+          // two chains per lane, row pairs split by lane half
+          nmc_ll_rows_lds<Fam, true>(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc,
+                                     &preg);
+          done = true;
+        }
+        if (!done)   // wave-uniform LDS address: broadcast ds_reads, pipelined
+          nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
       } else {          // rows beyond LDS: staged per wave by LDS-DMA, two chunks deep
         nmc_ll_rows_staged(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, glim,
                            lrows + (size_t)w * 2 * nmc_stage_buf(Fam::NFIELDS), acc);

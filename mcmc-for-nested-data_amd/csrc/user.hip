@@ -23,11 +23,17 @@
 namespace {
 
 // kernel table entries, in name-expression order
-enum { UK_RUN0 = 0, UK_NRUN = 5, UK_GROUP_LL = 5, UK_OBS_LL_ROWS = 6, UK_OBS_LL = 7, UK_N = 8 };
+// (step kernel: mode m with rows in LDS at UK_RUN0 + m, rows staged at UK_RUN0 + 5 + m)
+enum { UK_RUN0 = 0, UK_NRUN = 5, UK_GROUP_LL = 10, UK_OBS_LL_ROWS = 11, UK_OBS_LL = 12,
+       UK_N = 13 };
 const char* const kNames[UK_N] = {
-    "nmc_k_run<FamUser, 0>", "nmc_k_run<FamUser, 1>", "nmc_k_run<FamUser, 2>",
-    "nmc_k_run<FamUser, 3>", "nmc_k_run<FamUser, 4>", "nmc_k_group_ll<FamUser>",
-    "nmc_k_obs_ll_rows<FamUser>", "nmc_k_obs_ll<FamUser>"};
+    "nmc_k_run<FamUser, 0, true>", "nmc_k_run<FamUser, 1, true>", "nmc_k_run<FamUser, 2, true>",
+    "nmc_k_run<FamUser, 3, true>", "nmc_k_run<FamUser, 4, true>",
+    "nmc_k_run<FamUser, 0, false>", "nmc_k_run<FamUser, 1, false>",
+    "nmc_k_run<FamUser, 2, false>", "nmc_k_run<FamUser, 3, false>",
+    "nmc_k_run<FamUser, 4, false>", "nmc_k_group_ll<FamUser>", "nmc_k_obs_ll_rows<FamUser>",
+    "nmc_k_obs_ll<FamUser>"};
+int run_index(const nmc_ctx* x, int mode) { return UK_RUN0 + mode + (x->d.rows_lds ? 0 : UK_NRUN); }
 
 struct UserKernels {   // one device's modules, loaded on first use
   hipModule_t mod[UK_N] = {};
@@ -180,7 +186,7 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
         Dev dd = d;
         void* args[] = {&dd, &fam, (void*)&obs, &i0, &i1, &flags};
         hipFunction_t fr = nullptr;
-        rc = user_fn(x, UK_RUN0 + mode, &fr);
+        rc = user_fn(x, run_index(x, mode), &fr);
         if (!rc) rc = launch(x, fr, grid, block, lds, args);
       });
       return rc ? rc : e;
@@ -193,7 +199,7 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
       const int mode = x->d.hreg ? NMC_MODE_SYNC_REG
                                  : x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
       int nb = 0;
-      if (int rc = user_fn(x, UK_RUN0 + mode, &f)) return rc;
+      if (int rc = user_fn(x, run_index(x, mode), &f)) return rc;
       if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * x->d.W,
                                                             nmc_persist_lds(x)) != hipSuccess) {
         c.result = 0;
@@ -204,7 +210,7 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
     }
     case NMC_OP_CAPACITY: {
       int nb = 0;
-      if (int rc = user_fn(x, UK_RUN0 + run_mode(x), &f)) return rc;
+      if (int rc = user_fn(x, run_index(x, run_mode(x)), &f)) return rc;
       HIPCHK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f,
                                                                64 * x->d.W, run_lds_bytes(x)));
       c.result = nmc_safe_blocks(x, nb) * x->ncu;

@@ -11,7 +11,7 @@ import os
 import numpy
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("NESTMC_LIB", os.path.join(_HERE, "libnestmc.so"))
+LIB_PATH = os.environ.get("NESTMC_LIB") or os.path.join(_HERE, "libnestmc.so")
 
 POOLING = {"complete": 0, "none": 1, "partial": 2}
 FAMILY = {"linreg": 0, "gauss_mean": 1, "logistic": 2}
