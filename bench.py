@@ -246,6 +246,7 @@ def main():
     eng.event_record(0)
     t0 = time.perf_counter()
     eng.run(W, W + K)
+    t_enq = time.perf_counter() - t0          # host time to enqueue the launch(es)
     eng.event_record(1)
     eng.synchronize()
     t1 = time.perf_counter()
@@ -340,6 +341,8 @@ def main():
                          "pmc": pmc},
             "cpu_baseline": cpu,
             "event_ms": ev_ms,
+            "wall_ms": wall * 1e3,
+            "enqueue_ms": t_enq * 1e3,
             "hyper_only_avg_us": (kt["hyper_ms"] / max(1, kt["hyper_launches"])) * 1e3,
             "gather_ms": gather_ms,
         }

@@ -56,6 +56,7 @@ struct nmc_ctx {
   int* gidx = nullptr;                    // [n_obs] group of each observation (obs-LL rows)
   int64_t nmax_group = 0;                 // rows of the largest group
   int split_batch = 0;                    // row split: chain blocks per (resident) launch
+  bool tmo_clean = false;                 // timeout flag read clear, no launch since
   void* user = nullptr;                   // user family: its per-device kernel table (user.hip)
   double* user_k = nullptr;               // user family: device copy of the model constants
 };

@@ -169,6 +169,7 @@ static int check_timeout(nmc_ctx* x) {
   unsigned t = 0;
   HIPCHK(hipMemcpy(&t, x->d.tmo, sizeof(t), hipMemcpyDeviceToHost));
   if (t) return fail(-5, "persistent kernel: a chain-block wait timed out (workgroups not resident?)");
+  x->tmo_clean = true;   // no launch since this check (nmc_run skips its own)
   return 0;
 }
 
@@ -529,11 +530,12 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
   if (iter_begin == iter_end) return 0;
   if (x->rng == NMC_RNG_REPLAY && (!x->d.rz || iter_end > x->d.replay_n))
     return fail(-1, "replay variates do not cover the iteration range");
-  {   // a persistent launch that already timed out: stop before queueing more work
-    unsigned t = 0;
+  if (!x->tmo_clean) {   // a persistent launch that already timed out: stop before queueing
+    unsigned t = 0;     // more work (a synchronous read: skipped right after a synchronize)
     if (hipMemcpy(&t, x->d.tmo, sizeof(t), hipMemcpyDeviceToHost) == hipSuccess && t)
       return check_timeout(x);
   }
+  x->tmo_clean = false;
   const bool partial = x->pooling == NMC_POOL_PARTIAL;
   const int P = x->P;
   // the kernels read the values after iteration iter_begin-1 from vb[(iter_begin-1)&1]
