@@ -68,7 +68,8 @@ static inline size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
   // (register hand-off: no LDS payload buffers)
   return (size_t)nmc_lds(x->nacc, d.P, x->pooling == NMC_POOL_PARTIAL, d.nleaf, d.ntail, d.W,
                          d.G, hlds && !d.hreg,
-                         rows_lds ? d.nmax * x->nf : nmc_stage_doubles(x->nf, d.W))
+                         rows_lds ? d.nmax * x->nf
+                                  : (x->nf <= 4 ? 0 : nmc_stage_doubles(x->nf, d.W)))
              .total * 512;
 }
 static inline size_t pair_lds_bytes(const nmc_ctx* x) {

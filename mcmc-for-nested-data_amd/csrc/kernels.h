@@ -1417,8 +1417,8 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   // the Gibbs wave when it lands in the step that uses it (P <= 2)
   const int lag = hr && P >= 2 ? 2 : 1;
   // rows in LDS for the launch, or every wave's two staging buffers (nmc_ll_rows_staged)
-  const int row_doubles =
-      RL ? d.nmax * Fam::NFIELDS : nmc_stage_doubles(Fam::NFIELDS, blockDim.x >> 6);
+  const int row_doubles = RL ? d.nmax * Fam::NFIELDS
+                             : (Fam::NFIELDS <= 4 ? 0 : nmc_stage_doubles(Fam::NFIELDS, blockDim.x >> 6));
   const nmc_lds_layout L =
       nmc_lds(Fam::NACC, P, PARTIAL, d.nleaf, d.ntail, W, G, hl && !hr ? 1 : 0, row_doubles);
   double* th = lds + L.th * 64 + lane;            // th[p * 64]: this lane's chain, parameter p
@@ -1586,7 +1586,11 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         }
         if (!done)   // wave-uniform LDS address: broadcast ds_reads, pipelined
           nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
-      } else {          // rows beyond LDS: staged per wave by LDS-DMA, two chunks deep
+      } else if constexpr (Fam::NFIELDS <= 4) {
+        // rows beyond LDS, narrow rows: blocks of >= 4 rows per scalar load run ahead in
+        // the scalar cache (the staged loop measured 1.7x slower for 2-field rows)
+        nmc_ll_rows(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, acc);
+      } else {          // wide rows beyond LDS: staged per wave by LDS-DMA, two chunks deep
         nmc_ll_rows_staged(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, glim,
                            lrows + (size_t)w * 2 * nmc_stage_buf(Fam::NFIELDS), acc);
       }
