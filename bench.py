@@ -294,7 +294,7 @@ def main():
         traffic = pmc["bytes_per_launch"] * iters_per_launch / pmc["iterations_per_launch"]
         hbm_meas = traffic / (avg_step_ms * 1e-3) / 1e9
     lc = eng.launch_config()
-    kname = "nmc_k_run<FamLinreg<2>, %s>" % lc["mode"]
+    kname = lc["kernel"]
 
     if rank == 0:
         out = {

@@ -167,6 +167,9 @@ int nmc_launch_config(nmc_ctx* ctx, int* waves_per_group, int* chain_blocks, int
  * observation in ONE group): members = workgroups sharing each (chain block, group),
  * exchanging partial sums every step (1: no split); chain blocks per resident launch. */
 int nmc_split_config(nmc_ctx* ctx, int* members, int* chain_blocks_per_launch);
+/* The step kernel a run launches, e.g. "nmc_k_step<FamLinreg<2>, NMC_MODE_SYNC_REG>"
+ * (NUL-terminated, truncated to cap bytes); for the profiles and the bench report.    */
+int nmc_kernel_name(nmc_ctx* ctx, char* out, int cap);
 
 /* Sampler._printSample (:902-905) + _print (:933-936): append rows of local
  * chain c to a CSV file with the reference's "%i,%i,%f,..." formatting (and the

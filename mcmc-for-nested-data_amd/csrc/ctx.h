@@ -15,7 +15,7 @@
 
 #include "../../include/nestmc.h"
 #include "kernels.h"
-#include "pair.h"
+#include "step.h"
 
 // error message of the calling thread (nestmc.hip); returns code
 int nmc_fail(int code, const std::string& msg);
@@ -59,6 +59,7 @@ struct nmc_ctx {
   bool tmo_clean = false;                 // timeout flag read clear, no launch since
   void* user = nullptr;                   // user family: its per-device kernel table (user.hip)
   double* user_k = nullptr;               // user family: device copy of the model constants
+  bool step_ok = true;                    // nmc_k_step where it applies (NMC_STEP=0: nmc_k_run)
 };
 
 static inline double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->d.vb0; }
@@ -72,20 +73,26 @@ static inline size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
                                   : (x->nf <= 4 ? 0 : nmc_stage_doubles(x->nf, d.W)))
              .total * 512;
 }
-static inline size_t pair_lds_bytes(const nmc_ctx* x) {
-  return (size_t)nmc_pair_lds(x->nacc, x->d.nmax * x->nf).total * 512;
-}
-
 static inline int run_mode(const nmc_ctx* x) {
   if (x->pooling != NMC_POOL_PARTIAL) return NMC_MODE_NOPOOL;
   if (!x->persistent) return NMC_MODE_LAUNCH;
-  if (x->d.pair) return NMC_MODE_PAIR;
   if (x->d.hreg) return NMC_MODE_SYNC_REG;
   return x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
 }
 
+// The one-barrier step kernel (step.h) runs mode `mode` when the groups' rows are in LDS,
+// there is no row split, and the mode is none/complete pooling or the register hand-off.
+static inline bool uses_step(const nmc_ctx* x, int mode) {
+  return x->step_ok && x->d.rows_lds && x->d.S == 1 &&
+         (mode == NMC_MODE_NOPOOL || (mode == NMC_MODE_SYNC_REG && x->d.W >= 3));
+}
+static inline size_t step_lds_bytes(const nmc_ctx* x) {
+  return (size_t)nmc_step_lds(x->nacc, x->d.P, x->pooling == NMC_POOL_PARTIAL,
+                              x->d.nmax * x->nf).total * 512;
+}
+
 static inline size_t run_lds_bytes(const nmc_ctx* x) {
-  if (run_mode(x) == NMC_MODE_PAIR) return pair_lds_bytes(x);
+  if (uses_step(x, run_mode(x))) return step_lds_bytes(x);
   return lds_bytes_for(x, x->persistent && x->d.hlds ? 1 : 0, x->d.rows_lds);
 }
 
@@ -98,10 +105,20 @@ static inline int nmc_safe_blocks(const nmc_ctx* x, int nb) {
   const int W = x->d.W;
   return W % 4 == 0 ? std::min(nb, 24 / W) : (nb > 1 ? nb - 1 : nb);
 }
-static inline size_t pair_lds_bytes(const nmc_ctx* x);
+// mode of the persistent partial-pooling kernel (its occupancy query)
+static inline int nmc_persist_mode(const nmc_ctx* x) {
+  return x->d.hreg ? NMC_MODE_SYNC_REG : x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
+}
 // LDS of the persistent partial-pooling kernel (its occupancy query)
 static inline size_t nmc_persist_lds(const nmc_ctx* x) {
-  return x->d.pair ? pair_lds_bytes(x) : lds_bytes_for(x, x->d.hlds && !x->d.hreg, x->d.rows_lds);
+  if (uses_step(x, nmc_persist_mode(x))) return step_lds_bytes(x);
+  return lds_bytes_for(x, x->d.hlds && !x->d.hreg, x->d.rows_lds);
+}
+
+// dynamic LDS of nmc_k_group_part: the tile slots and (rows in LDS) the member's rows
+static inline size_t nmc_group_ll_lds(const nmc_ctx* x) {
+  const Dev& d = x->d;
+  return ((size_t)x->nacc * NMC_NSLOT + (d.rows_lds ? (d.nmax * x->nf + 63) / 64 + 1 : 0)) * 512;
 }
 
 static inline int pop_event_pair(nmc_ctx* x, std::vector<std::pair<hipEvent_t, hipEvent_t>>& v,
@@ -164,6 +181,7 @@ struct NmcCall {
   int i0 = 0, i1 = 0, flags = 0;
   const double* in = nullptr;
   double* out = nullptr;
+  double* aux = nullptr;   // op-specific device scratch
   int result = 0;
 };
 int nmc_call_linreg(nmc_ctx* x, NmcCall& c);

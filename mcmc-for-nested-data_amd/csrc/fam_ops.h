@@ -13,12 +13,14 @@ static const void* nmc_run_kernel_rl(int mode) {
     case NMC_MODE_LAUNCH: return (const void*)nmc_k_run<Fam, NMC_MODE_LAUNCH, RL>;
     case NMC_MODE_SYNC: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC, RL>;
     case NMC_MODE_SYNC_REG: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_REG, RL>;
-    case NMC_MODE_PAIR: return (const void*)nmc_k_pair<Fam>;
     default: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_LDS, RL>;
   }
 }
 template <class Fam>
 static const void* nmc_run_kernel(const nmc_ctx* x, int mode) {
+  if (uses_step(x, mode))
+    return mode == NMC_MODE_NOPOOL ? (const void*)nmc_k_step<Fam, NMC_MODE_NOPOOL>
+                                   : (const void*)nmc_k_step<Fam, NMC_MODE_SYNC_REG>;
   return x->d.rows_lds ? nmc_run_kernel_rl<Fam, true>(mode) : nmc_run_kernel_rl<Fam, false>(mode);
 }
 
@@ -39,10 +41,7 @@ template <class Fam>
 static bool nmc_can_persist(nmc_ctx* x) {
   if (const char* e = getenv("NMC_PERSIST")) return atoi(e) != 0;
   int nb = 0;
-  const void* k = nmc_run_kernel<Fam>(x, x->d.pair   ? NMC_MODE_PAIR
-                                         : x->d.hreg ? NMC_MODE_SYNC_REG
-                                         : x->d.hlds ? NMC_MODE_SYNC_LDS
-                                                     : NMC_MODE_SYNC);
+  const void* k = nmc_run_kernel<Fam>(x, nmc_persist_mode(x));
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W, nmc_persist_lds(x)) !=
       hipSuccess)
     return false;
@@ -66,10 +65,20 @@ static int nmc_fam_call(nmc_ctx* x, const Fam& fam, NmcCall& c) {
       c.result = nmc_safe_blocks(x, nb) * x->ncu;
       return 0;
     }
-    case NMC_OP_GROUP_LL: {
-      const size_t lds = (size_t)x->d.W * 64 * Fam::NACC * sizeof(double);
-      hipLaunchKernelGGL(nmc_k_group_ll<Fam>, dim3(x->d.CB * x->G), dim3(64 * x->d.W), lds,
-                         x->stream, x->d, fam, x->d.obs, c.in, c.out);
+    case NMC_OP_GROUP_LL: {   // c.aux: [S][NACC][G][C] member partials
+      const Dev& d = x->d;
+      const size_t lds = nmc_group_ll_lds(x);
+      const void* k = d.rows_lds ? (const void*)nmc_k_group_part<Fam, true>
+                                 : (const void*)nmc_k_group_part<Fam, false>;
+      Dev dd = d;
+      const double* obs = d.obs;
+      const double* in = c.in;
+      double* aux = c.aux;
+      void* a1[] = {&dd, (void*)&fam, (void*)&obs, (void*)&in, (void*)&aux};
+      HIPCHK(hipLaunchKernel(k, dim3(d.CB * d.G * d.S), dim3(64 * d.W), a1, lds, x->stream));
+      const size_t n = (size_t)d.G * d.C;
+      hipLaunchKernelGGL(nmc_k_group_fin<Fam>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                         x->stream, d, fam, c.in, (const double*)c.aux, c.out);
       HIPCHK(hipGetLastError());
       return 0;
     }

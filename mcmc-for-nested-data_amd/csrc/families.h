@@ -24,6 +24,16 @@
 
 #define NMC_MAXP 16
 
+// numpy.logaddexp(0, eta) (npy_logaddexp: x == y -> x + ln 2; else max + log1p(exp(-|x - y|)),
+// NaN propagating), branch-free: one exp and one log1p per lane whatever the sign of eta, so
+// lanes whose eta differ in sign do not run both halves.  Bit-identical to the branchy form:
+// eta < 0 gives 0.0 + log1p(exp(eta)) == log1p(exp(eta)); +-inf give inf / 0; NaN gives NaN.
+__device__ __forceinline__ double nmc_logaddexp0(double eta) {
+  const double m = eta > 0.0 ? eta : 0.0;
+  const double r = m + log1p(exp(-fabs(eta)));
+  return eta == 0.0 ? NMC_LN2 : r;
+}
+
 // ---------------------------------------------------------------------------
 // Gaussian linear regression (example/regression.py:53-67; cfg 3/4 with sigma=1):
 //   rows [x_1..x_K, y] (K = NF-1); params [b0 if intercept, b_1..b_K, sigma if
@@ -203,11 +213,7 @@ struct FamLogistic {
     for (int j = 0; j < K; ++j) r.b[j] = intercept ? th[j + 1] : th[j];
     return r;
   }
-  __device__ __forceinline__ static double logaddexp0(double eta) {
-    // numpy.logaddexp(0, eta): max + log1p(exp(-|diff|)); NaN propagates
-    if (eta == 0.0) return NMC_LN2;
-    return eta > 0.0 ? eta + log1p(exp(-eta)) : log1p(exp(eta));
-  }
+  __device__ __forceinline__ static double logaddexp0(double eta) { return nmc_logaddexp0(eta); }
   __device__ __forceinline__ void accum(const Reg& r, const double* __restrict__ row,
                                         double* acc) const {
     double eta = r.b0;

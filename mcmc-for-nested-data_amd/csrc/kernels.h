@@ -54,8 +54,6 @@ struct Dev {
   // cfg 3 and was removed.)
   int CL, RB;
   int paired;            // likelihood rows: two chains per lane (nmc_ll_rows_lds<Fam, true>)
-  int vzin;              // Philox step variates drawn in the step kernel (not by nmc_k_fill)
-  int gtiles;            // register Gibbs mode: the Gibbs wave takes likelihood tiles too
   // Row split (none/complete pooling with large groups): S workgroups ("members") share
   // one (chain block, group), member m owning the m-th contiguous chunk of the group's
   // rows (nmc_chunk); each step they exchange their partial sums through xbuf
@@ -64,6 +62,10 @@ struct Dev {
   // count only, never on the chain count: results are shard- and batch-invariant.
   // cb0: first chain block of this launch (chain blocks are launched in resident batches).
   int S, cb0;
+  // publish / exchange counters are never reset between launches: they already hold
+  // G * pbase publishes per (chain block, parameter) and S * xbase arrivals per unit from
+  // the context's earlier launches (the host advances both; no memset per launch)
+  unsigned pbase, xbase;
   double* xbuf;
   unsigned* xcnt;
   uint32_t seed;
@@ -91,7 +93,6 @@ struct Dev {
   int nmax;              // rows of the largest group
   int hlds, naux;        // persistent partial: Gibbs payload via LDS, auxiliary waves
   int hreg;              // persistent partial, G <= 64: Gibbs payload in registers (SYNC_REG)
-  int pair;              // persistent partial, G <= 64, P == 2: the pair kernel (pair.h)
   int noprio;            // diagnostics: no issue priority for the latency-bound waves
   int rows_lds;          // 1: each workgroup stages its group's rows in LDS once per launch
   int tile;              // target rows per likelihood tile (nmc_tiles)
@@ -190,6 +191,8 @@ enum { NMC_RUN_HYPER_LOAD = 1 };
 #endif
 enum { NMC_NSLOT = NMC_NSLOT_N };
 enum { NMC_SPIN_LIMIT = 1 << 22 };
+// CU count the row split is sized for (a full MI355X), whatever the device reports
+enum { NMC_SPLIT_CU_BASIS = 256 };
 
 // Offset of the hyper-parameter slot holding the state after iteration t ([2][P][C]:
 // slot t & 1, like the values vb[t & 1]); a launch reads one slot and writes the other.
@@ -489,6 +492,7 @@ __device__ __forceinline__ unsigned* nmc_counter(const Dev& d, int cb, int p, in
 }
 __device__ __forceinline__ bool nmc_poll_published(const Dev& d, int cb, int p, unsigned target) {
   const int lane = threadIdx.x & 63;
+  target += (unsigned)d.G * d.pbase;   // (counts of the context's earlier launches)
   unsigned* ctr = nmc_counter(d, cb, p, lane & 7);
   for (unsigned spins = 0;; ++spins) {
     const unsigned v =
@@ -509,16 +513,20 @@ __device__ __forceinline__ bool nmc_poll_published(const Dev& d, int cb, int p, 
 }
 
 // Whole-workgroup wait (thread 0 polls, result broadcast through LDS).
-__device__ __forceinline__ bool nmc_wait_published(const Dev& d, int cb, int p, unsigned target,
-                                                   double* lds, const nmc_lds_layout& L) {
+__device__ __forceinline__ bool nmc_wait_published_col(const Dev& d, int cb, int p,
+                                                       unsigned target, double* lds, int flagcol) {
   if (threadIdx.x < 64) {
     const bool r = nmc_poll_published(d, cb, p, target);
-    if (threadIdx.x == 0) lds[L.flag * 64] = r ? 1.0 : 0.0;
+    if (threadIdx.x == 0) lds[flagcol * 64] = r ? 1.0 : 0.0;
   }
   __syncthreads();
   // keep the payload loads below the poll (no instruction: wavefront scope)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  return lds[L.flag * 64] != 0.0;
+  return lds[flagcol * 64] != 0.0;
+}
+__device__ __forceinline__ bool nmc_wait_published(const Dev& d, int cb, int p, unsigned target,
+                                                   double* lds, const nmc_lds_layout& L) {
+  return nmc_wait_published_col(d, cb, p, target, lds, L.flag);
 }
 
 // ---------------------------------------------------------------------------
@@ -527,12 +535,19 @@ __device__ __forceinline__ bool nmc_wait_published(const Dev& d, int cb, int p, 
 // LDS), R rows (~BLK doubles) per block, four accumulator sets to break the
 // dependence chain.
 // ---------------------------------------------------------------------------
-template <class Fam, int BLK = 16>
+// rows per block of the global-memory / staged row loops: >= 4 rows of narrow rows (the
+// scalar-load loop runs ahead in the scalar cache), 4 rows of 5-8 fields (four independent
+// per-row chains -- e.g. logistic's exp / log1p -- in flight per lane), fewer for wider rows
+// (registers)
+__host__ __device__ constexpr int nmc_row_block(int nf) {
+  return nf <= 4 ? 16 / nf : (32 / nf >= 4 ? 4 : (32 / nf > 0 ? 32 / nf : 1));
+}
+template <class Fam>
 __device__ __forceinline__ void nmc_ll_rows(const Fam& fam, const typename Fam::Reg& reg,
                                             const double* __restrict__ p, int n,
                                             double (&acc)[Fam::NACC]) {
   constexpr int NF = Fam::NFIELDS;
-  constexpr int R = (BLK / NF) > 0 ? (BLK / NF) : 1;
+  constexpr int R = nmc_row_block(NF);
   double a[4][Fam::NACC];
 #pragma unroll
   for (int s = 0; s < 4; ++s)
@@ -827,7 +842,6 @@ __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename F
 // round trip per row for the scalar-load loop it replaces -- hides behind the arithmetic.
 // Same R-row blocks, accumulators and order as nmc_ll_rows (bit-identical sums).
 // ---------------------------------------------------------------------------
-__host__ __device__ constexpr int nmc_row_block(int nf) { return (16 / nf) > 0 ? 16 / nf : 1; }
 // rows per chunk: as many whole row blocks as one 1 KiB DMA instruction carries beside
 // 16 B of alignment slack (n_fields <= 64: at least one row)
 __host__ __device__ constexpr int nmc_stage_rows(int nf) {
@@ -1166,8 +1180,7 @@ __device__ __forceinline__ void nmc_hyper_compute_reg(const Dev& d, int cb, int 
                                                       double hz, double hx,
                                                       const double (&x)[64]) {
   const int lane = threadIdx.x & 63;
-  const int P = d.P, G = d.G, C = d.C;
-  const int c = nmc_lane_chain(d, cb, lane);
+  const int P = d.P, G = d.G;
   double* hy = lds + hyp * 64 + lane;
   const double sdm = sqrt(hy[(NMC_HY_S2 * P + p) * 64] / G);
   const double tot = nmc_pairwise_reg(x, G, false, 0.0);
@@ -1239,7 +1252,7 @@ __device__ __forceinline__ void nmc_split_exchange(const Dev& d, int cb, int g, 
   const int lane = threadIdx.x & 63;
   const int S = d.S;
   const size_t unit = (size_t)cb * d.G + g;
-  double* xb = d.xbuf + (((size_t)(k & 1) * d.RB * d.G + unit) * S) * NA * 64 + lane;
+  double* xb = d.xbuf + (((size_t)((k + d.xbase) & 1) * d.RB * d.G + unit) * S) * NA * 64 + lane;
 #pragma unroll
   for (int j = 0; j < NA; ++j)
     __hip_atomic_store(xb + ((size_t)m * NA + j) * 64, acc[j], __ATOMIC_RELAXED,
@@ -1247,7 +1260,7 @@ __device__ __forceinline__ void nmc_split_exchange(const Dev& d, int cb, int g, 
   nmc_drain_vm();
   unsigned* ctr = d.xcnt + unit * 32;
   if (lane == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned target = (unsigned)S * (unsigned)(k + 1);
+  const unsigned target = (unsigned)S * ((unsigned)k + d.xbase + 1u);
   for (unsigned spins = 0;; ++spins) {
     const unsigned v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (v >= target) break;
@@ -1382,10 +1395,8 @@ enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
        NMC_MODE_LAUNCH = 1,      // one launch per iteration, plain loads after the boundary
        NMC_MODE_SYNC = 2,        // persistent, sc1 loads after the barrier
        NMC_MODE_SYNC_LDS = 3,    // persistent, the Gibbs wave works on an LDS copy
-       NMC_MODE_SYNC_REG = 4,    // persistent, G <= 64: the Gibbs wave fetches the task's
+       NMC_MODE_SYNC_REG = 4 };  // persistent, G <= 64: the Gibbs wave fetches the task's
                                  // values straight into registers and updates in one step
-       NMC_MODE_PAIR = 5 };      // persistent, G <= 64, P == 2: both steps of an iteration
-                                 // from one pass over the rows (pair.h, nmc_k_pair)
 // RL: the groups' rows are staged in LDS for the launch (d.rows_lds) -- a template
 // parameter so each instance holds only its own row loop (the LDS-DMA staged loop's
 // registers raised the rows-in-LDS kernel's pressure: ~5 % of its time at cfg 3)
@@ -1475,20 +1486,9 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   auto zl_src = [&](int tn, int pn) -> const double* {
     return d.vzl + ((size_t)(tn - d.vbase) * PGC + (size_t)pn * G * C + gc) * 2;
   };
-  // {z, log u} of step (tn, pn) -> LDS slot: Philox drawn here by the control wave
-  // (d.vzin: nmc_k_fill's formulas, no HBM round trip), or LDS-DMA of the replayed
-  // variates nmc_k_fill wrote
+  // {z, log u} of step (tn, pn) -> LDS slot: LDS-DMA of the variates nmc_k_fill wrote
   auto put_zl = [&](int tn, int pn, int slot) {
-    double* z = lds + (L.zl + 2 * slot) * 64;
-    if (d.vzin) {
-      const uint32_t ch = (uint32_t)(d.chain_base + cc);
-      const double zz = nmc_normal(tn, g, pn, NMC_PURPOSE_PROPOSAL, ch, d.seed);
-      const double lu = log(nmc_uniform2(tn, g, pn, NMC_PURPOSE_ACCEPT, ch, d.seed).a);
-      z[2 * lane] = zz;
-      z[2 * lane + 1] = lu;
-    } else {
-      nmc_dma16(zl_src(tn, pn), z);
-    }
+    nmc_dma16(zl_src(tn, pn), lds + (L.zl + 2 * slot) * 64);
   };
   double* cwv = lds + L.cw * 64 + lane;    // cwv[k * 64]: control-wave values across barriers
   if (ctl) {     // {z, log u} of the first step -> LDS slot of step i0*P
@@ -1635,7 +1635,6 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             }
           }
         }
-        if (d.gtiles) lik_tiles(t, p, gs & 1, []() {});
         __syncthreads();   // A
         if (due) {
           ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
@@ -1967,38 +1966,85 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   }
 }
 
-// Group sums for arbitrary theta [P][G][C] -> out [G][C] (all W waves stream rows).
-template <class Fam>
-__global__ void __launch_bounds__(1024)
-nmc_k_group_ll(Dev d, Fam fam, const double* __restrict__ obs, const double* theta,
-               double* out) {
-  extern __shared__ __attribute__((aligned(16))) double red[];
+// Group log-likelihoods for arbitrary theta [P][G][C] (the batched start-point search and
+// partial init of nestmc/init.py), summed EXACTLY as the step kernels sum a proposal's
+// likelihood: the same row-split members, tile partition (nmc_tiles), row loop (rows
+// staged in LDS or read from global memory, as the step kernel of this context does),
+// 16-slot combine, member order and finish_fast -- so a chain's stored group LL never
+// depends on which kernel produced it, on the wave count or on the chain sharding.
+// Part 1: grid CB * G * S workgroups (member m of group g of chain block cb), W waves take
+// tiles k = w, w + W, ...; out part[m][j][g][C] (NACC accumulators).
+template <class Fam, bool RL>
+__global__ void __launch_bounds__(512)
+nmc_k_group_part(Dev d, Fam fam, const double* __restrict__ obs, const double* theta,
+                 double* part) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // [NACC][NSLOT] slots, rows
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int W = blockDim.x >> 6;
-  const int g = blockIdx.x % d.G, cb = blockIdx.x / d.G;
+  const int S = d.S;
+  const int mb = blockIdx.x % S;
+  const int g = (blockIdx.x / S) % d.G, cb = (blockIdx.x / S) / d.G;
   const int c = cb * 64 + lane;
   const int cc = c < d.C ? c : d.C - 1;
   double th[Fam::MAXP];
   nmc_load_theta(d, theta, g, cc, th);
   const typename Fam::Reg reg = fam.prepare(th);
-  const int64_t r0 = d.off[g], r1 = d.off[g + 1];
-  int64_t a;
-  int n;
-  nmc_chunk(r0, r1, w, W, &a, &n);
-  double acc[Fam::NACC];
-  nmc_ll_rows(fam, reg, obs + a * Fam::NFIELDS, n, acc);
+  int64_t r0;
+  int nrow;
+  nmc_chunk(d.off[g], d.off[g + 1], mb, S, &r0, &nrow);
+  const nmc_tiling TI = nmc_tiles(nrow, d.tile);
+  const double* grows = obs + r0 * Fam::NFIELDS;
+  double* lrows = lds + Fam::NACC * NMC_NSLOT * 64;
+  if constexpr (RL) {
+    const int nd = nrow * Fam::NFIELDS;
+    for (int i = threadIdx.x; i < nd; i += blockDim.x) lrows[i] = grows[i];
+  }
+  for (int j = 0; j < Fam::NACC; ++j)
+    for (int k = TI.nt + w; k < NMC_NSLOT; k += W) lds[(j * NMC_NSLOT + k) * 64 + lane] = -0.0;
+  __syncthreads();
+  for (int k = w; k < TI.nt; k += W) {
+    const int ra = TI.start(k), rn = TI.len(k);
+    double acc[Fam::NACC];
+    if constexpr (RL)
+      nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
+    else
+      nmc_ll_rows(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, acc);
 #pragma unroll
-  for (int j = 0; j < Fam::NACC; ++j) red[(j * W + w) * 64 + lane] = acc[j];
+    for (int j = 0; j < Fam::NACC; ++j) lds[(j * NMC_NSLOT + k) * 64 + lane] = acc[j];
+  }
   __syncthreads();
   if (w != 0 || c >= d.C) return;
 #pragma unroll
+  for (int j = 0; j < Fam::NACC; ++j)
+    part[(((size_t)mb * Fam::NACC + j) * d.G + g) * d.C + c] = nmc_sum_slots(lds + j * NMC_NSLOT * 64 + lane);
+}
+
+// Part 2: the members' partials in member order (nmc_split_exchange's four streams),
+// finish_fast -> out [G][C].  One thread per (group, chain).
+template <class Fam>
+__global__ void __launch_bounds__(256)
+nmc_k_group_fin(Dev d, Fam fam, const double* theta, const double* part, double* out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)d.G * d.C) return;
+  const int c = (int)(i % d.C), g = (int)(i / d.C);
+  const int S = d.S;
+  double th[Fam::MAXP];
+  nmc_load_theta(d, theta, g, c, th);
+  const typename Fam::Reg reg = fam.prepare(th);
+  double acc[Fam::NACC];
+#pragma unroll
   for (int j = 0; j < Fam::NACC; ++j) {
-    double sum = red[(j * W) * 64 + lane];
-    for (int u = 1; u < W; ++u) sum += red[(j * W + u) * 64 + lane];
-    acc[j] = sum;
+    double s4[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int m = 0; m < S; ++m) {
+      const double v = part[(((size_t)m * Fam::NACC + j) * d.G + g) * d.C + c];
+      s4[m & 3] = m < 4 ? v : s4[m & 3] + v;
+    }
+    acc[j] = S >= 4 ? (s4[0] + s4[1]) + (s4[2] + s4[3])
+                    : (S == 1 ? s4[0] : (S == 2 ? s4[0] + s4[1] : (s4[0] + s4[1]) + s4[2]));
   }
-  out[(size_t)g * d.C + c] = fam.finish(reg, acc, (long)(r1 - r0));
+  const long n = (long)(d.off[g + 1] - d.off[g]);
+  out[i] = fam.finish_fast(reg, acc, n, fam.gconst(n));
 }
 
 // StepMethod.logLikelihood (:656-659) at recorded rows of the device sample store:

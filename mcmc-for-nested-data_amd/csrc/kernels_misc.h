@@ -10,7 +10,7 @@
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) nmc_k_fill(Dev d, int iter0, int T) {
   const size_t PGC = (size_t)d.P * d.G * d.C, PC = (size_t)d.P * d.C;
-  const size_t n1 = d.vzin ? 0 : (size_t)T * PGC;   // (vzin: the step kernel draws them)
+  const size_t n1 = (size_t)T * PGC;
   const size_t n2 = d.pooling == NMC_POOL_PARTIAL ? (size_t)T * PC : 0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n1 + n2;
        i += (size_t)gridDim.x * blockDim.x) {

@@ -68,17 +68,21 @@ static void choose_geometry(nmc_ctx* x) {
   }
   d.RB = (d.C + d.CL - 1) / d.CL;
   d.W = (int)w;
-  d.tile = 64;   // rows per likelihood tile (a multiple of 16); diagnostics override below
+  d.tile = 64;   // rows per likelihood tile (a multiple of 16)
+#ifdef NMC_DEBUG_KNOBS   // (diagnostic builds only: changes the summation order)
   if (const char* e = getenv("NMC_TILE_ROWS")) {
     const int v = atoi(e);
     if (v >= 16 && v % 16 == 0) d.tile = v;
   }
+#endif
   // partial pooling, persistent payload-in-LDS mode: wave 1 is the Gibbs wave
   d.naux = x->pooling == NMC_POOL_PARTIAL && d.W >= 3 && d.G <= 256 ? 1 : 0;
   // rows in LDS when they fit beside the rest of the carve (64 KiB for the rows)
   d.rows_lds = (size_t)d.nmax * x->nf * 8 <= (size_t)64 * 1024 &&
-               lds_bytes_for(x, 0, 1) <= (size_t)96 * 1024 &&
-               !(getenv("NMC_NO_LDS_ROWS") && atoi(getenv("NMC_NO_LDS_ROWS")));
+               lds_bytes_for(x, 0, 1) <= (size_t)96 * 1024;
+#ifdef NMC_DEBUG_KNOBS   // (diagnostic builds only: the scalar-load row loop's blocks differ)
+  if (getenv("NMC_NO_LDS_ROWS") && atoi(getenv("NMC_NO_LDS_ROWS"))) d.rows_lds = 0;
+#endif
 
   // the persistent Gibbs update by the auxiliary waves needs G <= 128 (one numpy
   // leaf) and one parameter's chain-block values in LDS
@@ -94,25 +98,6 @@ static void choose_geometry(nmc_ctx* x) {
   const bool stream = getenv("NMC_HREG_STREAM") && atoi(getenv("NMC_HREG_STREAM"));
   d.hreg = d.naux > 0 && (d.G <= 64 ? d.hlds : stream && d.nleaf <= 4) &&
            !(getenv("NMC_NO_HREG") && atoi(getenv("NMC_NO_HREG")));
-  // P == 2 with rows in LDS: both steps of an iteration from one pass (pair.h); needs
-  // the control wave, two Gibbs waves and at least one likelihood wave
-  // (measured on MI355X at cfg 3: 8.6-9.8 us per iteration against 8.0 for SYNC_REG --
-  // the three-sum pass is VALU-bound with two of the four SIMDs holding a Gibbs wave --
-  // so it is opt-in, NMC_PAIR=1, for the measurements in DESIGN.md)
-  d.pair = d.hreg && d.P == 2 && d.rows_lds && x->family < NMC_LL_USER_BASE &&
-           (size_t)nmc_pair_lds(x->nacc, d.nmax * x->nf).total * 512 <= (size_t)160 * 1024 &&
-           getenv("NMC_PAIR") && atoi(getenv("NMC_PAIR"));
-  if (d.pair && d.W < 4) d.W = 4;
-  // Philox step variates drawn in the step kernel's control-wave slack instead of by
-  // nmc_k_fill (NMC_VZIN=1; Philox mode, not the pair kernel).  Measured on MI355X at
-  // cfg 3: 8.97 us/iter against 8.59 with the fill -- Box-Muller's fp64 log/sqrt/cos on
-  // the control wave's critical path costs more than the fill's 524 KB round trip -- so
-  // the fill stays the default.
-  d.vzin = 0;
-  d.gtiles = 0;   // (NMC_GIBBS_TILES=1: measured no better at cfg 3)
-  if (const char* e = getenv("NMC_GIBBS_TILES")) d.gtiles = atoi(e) != 0;
-  if (const char* e = getenv("NMC_VZIN"))
-    d.vzin = x->rng == NMC_RNG_PHILOX && !d.pair && atoi(e) != 0;
   // Partial pooling whose grid is more than one 8-wave workgroup per CU but fits two
   // 4-wave ones (cfg-4 shards: 2 chain blocks x 256 groups): four waves, so the whole
   // grid is resident and runs persistent (both chain blocks' workgroups share each CU
@@ -131,6 +116,9 @@ static void choose_geometry(nmc_ctx* x) {
   // reads; NMC_ROWS=bcast keeps the one-chain broadcast loop (same sums bit for bit)
   d.paired = d.rows_lds && x->nf <= 4;
   if (const char* e = getenv("NMC_ROWS")) d.paired = d.paired && strcmp(e, "bcast") != 0;
+  // the one-barrier step kernel (step.h) where it applies; NMC_STEP=0 keeps nmc_k_run
+  // (bit-identical: the tests compare the two)
+  x->step_ok = !(getenv("NMC_STEP") && atoi(getenv("NMC_STEP")) == 0);
 }
 
 // numpy's pairwise-sum recursion over G groups (numpy/_core/src/umath/loops_utils.h):
@@ -163,6 +151,11 @@ static int launch_hyper(nmc_ctx* x, int t) {
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev->second, x->stream));
   return 0;
+}
+
+// publish counters [RB <= ceil(C / 32)][P][8 shards][32]
+static size_t cnt_bytes(const nmc_ctx* x) {
+  return (size_t)32 * 8 * ((x->C + 31) / 32) * x->P * sizeof(unsigned);
 }
 
 static int check_timeout(nmc_ctx* x) {
@@ -303,9 +296,11 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   rc |= dalloc(x, &dleaf, starts.size());
   rc |= dalloc(x, &dmerge, merges.size());
   // [RB][P][8 shards][32], RB <= ceil(C / 32)
-  rc |= dalloc(x, &d.cnt, (size_t)32 * 8 * ((n_chains + 31) / 32) * n_params);
+  rc |= dalloc(x, &d.cnt, cnt_bytes(x) / sizeof(unsigned));
   rc |= dalloc(x, &d.tmo, 4);
   if (rc) { nmc_destroy(x); return rc; }
+  HIPCHK(hipMemset(d.cnt, 0, cnt_bytes(x)));
+  d.pbase = d.xbase = 0;
   d.leaf = dleaf;
   d.merge = dmerge;
   HIPCHK(hipMemcpy(dleaf, starts.data(), starts.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -317,20 +312,24 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     nmax = std::max<int64_t>(nmax, group_offsets[g + 1] - group_offsets[g]);
   x->nmax_group = nmax;
   // Row split: groups far larger than one workgroup's 64 KiB LDS row area are shared by S
-  // workgroups, at most 64 and at most one per CU per group.  S depends on (rows,
-  // fields, groups, CU count) only -- never on the chain count -- so the partial-sum
-  // order, and every result, is the same whatever the sharding or launch batching.
+  // workgroups, at most 64 and at most one per CU of a full MI355X (256 CUs) per group.
+  // S depends on (rows, fields, groups) only -- never on the chain count or on the
+  // device's CU count -- so the partial-sum order, and every result, is the same whatever
+  // the sharding, the launch batching or the GPU partition (a partition too small to
+  // hold the S members of one group at once refuses the run: nmc_create below).
   d.S = 1;
   d.cb0 = 0;
   {
     const int64_t target = std::max<int64_t>(256, (64 * 1024) / (n_fields * 8));
     if (nmax > 2 * target)
       d.S = (int)std::min<int64_t>({64, (nmax + target - 1) / target,
-                                    std::max<int64_t>(1, x->ncu / n_groups)});
+                                    std::max<int64_t>(1, NMC_SPLIT_CU_BASIS / n_groups)});
+#ifdef NMC_DEBUG_KNOBS   // (diagnostic builds only: changes the summation order)
     if (const char* e = getenv("NMC_SPLIT")) {
       const int v = atoi(e);
       if (v >= 1 && v <= 256) d.S = v;
     }
+#endif
   }
   d.nmax = (int)((nmax + d.S - 1) / d.S);   // rows of the largest member
   choose_geometry(x);
@@ -364,6 +363,7 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     rc |= dalloc(x, &d.xbuf, (size_t)2 * d.RB * d.G * d.S * x->nacc * 64);
     rc |= dalloc(x, &d.xcnt, (size_t)d.RB * d.G * 32);
     if (rc) { nmc_destroy(x); return rc; }
+    HIPCHK(hipMemset(d.xcnt, 0, (size_t)d.RB * d.G * 32 * sizeof(unsigned)));
   }
   d.thin = 1; d.tune_interval = 100;
   HIPCHK(hipMemcpy(off, group_offsets, (n_groups + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
@@ -567,24 +567,30 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       // every variate of iterations [c0, c1) in one fully parallel launch
       x->d.vbase = c0;
       const size_t n =
-          (size_t)(c1 - c0) * P * x->C * ((x->d.vzin ? 0 : x->G) + (partial ? 1 : 0));
+          (size_t)(c1 - c0) * P * x->C * (x->G + (partial ? 1 : 0));
       if (n) {
         const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);
         hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);
         HIPCHK(hipGetLastError());
       }
+      // counters continue from the earlier launches (Dev.pbase / xbase): reset only
+      // before they could wrap
+      const uint64_t steps = (uint64_t)(c1 - c0) * P;
+      if ((uint64_t)x->G * (x->d.pbase + (uint64_t)(c1 - c0)) >= (1ull << 31) ||
+          (uint64_t)x->d.S * (x->d.xbase + steps) >= (1ull << 31)) {
+        HIPCHK(hipMemsetAsync(x->d.cnt, 0, cnt_bytes(x), x->stream));
+        if (x->d.xcnt)
+          HIPCHK(hipMemsetAsync(x->d.xcnt, 0, (size_t)x->d.RB * x->d.G * 32 * sizeof(unsigned),
+                                x->stream));
+        x->d.pbase = x->d.xbase = 0;
+      }
       if (!partial) {
-        if (x->d.S > 1)   // row split: fresh exchange counters for the launch
-          HIPCHK(hipMemsetAsync(x->d.xcnt, 0, (size_t)x->d.RB * x->d.G * 32 * sizeof(unsigned),
-                                x->stream));
         if (int rc = launch_run(c0, c1, 0)) return rc;
+        x->d.xbase += (unsigned)steps;
       } else if (x->persistent) {
-        HIPCHK(hipMemsetAsync(x->d.cnt, 0, (size_t)32 * 8 * x->d.RB * x->P * sizeof(unsigned),
-                              x->stream));
-        if (x->d.S > 1)
-          HIPCHK(hipMemsetAsync(x->d.xcnt, 0, (size_t)x->d.RB * x->d.G * 32 * sizeof(unsigned),
-                                x->stream));
         if (int rc = launch_run(c0, c1, NMC_RUN_HYPER_LOAD)) return rc;
+        x->d.pbase += (unsigned)(c1 - c0);
+        x->d.xbase += (unsigned)steps;
       } else {
         for (int it = c0; it < c1; ++it)
           if (int rc = launch_run(it, it + 1, it == c0 ? NMC_RUN_HYPER_LOAD : 0)) return rc;
@@ -627,22 +633,26 @@ int nmc_get_accept_counts(nmc_ctx* x, int64_t* out) {
 int nmc_eval_group_ll(nmc_ctx* x, const double* theta, double* out) {
   hipSetDevice(x->device);
   const size_t PGC = (size_t)x->P * x->G * x->C, GC = (size_t)x->G * x->C;
-  double *th = nullptr, *o = nullptr;
+  double *th = nullptr, *o = nullptr, *part = nullptr;
   HIPCHK(hipMalloc(&th, PGC * 8));
   HIPCHK(hipMalloc(&o, GC * 8));
+  HIPCHK(hipMalloc(&part, (size_t)x->d.S * x->nacc * GC * 8));
   HIPCHK(hipMemcpyAsync(th, theta, PGC * 8, hipMemcpyHostToDevice, x->stream));
   NmcCall c;
   c.op = NMC_OP_GROUP_LL;
   c.in = th;
   c.out = o;
+  c.aux = part;
   int rc = nmc_call_family(x, c);
   if (!rc) {
     hipError_t e = hipMemcpyAsync(out, o, GC * 8, hipMemcpyDeviceToHost, x->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(x->stream);
     if (e != hipSuccess) rc = fail(-2, std::string("eval_group_ll: ") + hipGetErrorString(e));
   }
+  hipStreamSynchronize(x->stream);
   hipFree(th);
   hipFree(o);
+  hipFree(part);
   return rc;
 }
 
@@ -725,6 +735,26 @@ int nmc_get_kernel_timing(nmc_ctx* x, double* step_ms, int64_t* step_n, int64_t*
 int nmc_split_config(nmc_ctx* x, int* members, int* chain_blocks_per_launch) {
   *members = x->d.S;
   *chain_blocks_per_launch = x->d.S > 1 ? x->split_batch : x->d.RB;
+  return 0;
+}
+
+int nmc_kernel_name(nmc_ctx* x, char* out, int cap) {
+  static const char* const modes[] = {"NMC_MODE_NOPOOL", "NMC_MODE_LAUNCH", "NMC_MODE_SYNC",
+                                      "NMC_MODE_SYNC_LDS", "NMC_MODE_SYNC_REG"};
+  const int mode = run_mode(x);
+  std::string fam;
+  switch (x->family) {
+    case NMC_LL_LINREG: fam = "FamLinreg<" + std::to_string(x->nf) + ">"; break;
+    case NMC_LL_GAUSS_MEAN: fam = "FamGaussMean<" + std::to_string(x->nf) + ">"; break;
+    case NMC_LL_LOGISTIC: fam = "FamLogistic<" + std::to_string(x->nf) + ">"; break;
+    default: fam = "FamUser"; break;
+  }
+  std::string k = uses_step(x, mode)
+                      ? "nmc_k_step<" + fam + ", " + modes[mode] + ">"
+                      : "nmc_k_run<" + fam + ", " + modes[mode] + ", " +
+                            (x->d.rows_lds ? "true" : "false") + ">";
+  if (cap < 1) return fail(-1, "kernel name: cap < 1");
+  snprintf(out, (size_t)cap, "%s", k.c_str());
   return 0;
 }
 

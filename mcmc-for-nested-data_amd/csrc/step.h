@@ -1,0 +1,409 @@
+// step.h -- the one-barrier step kernel: nmc_k_step<Fam, MODE>, the production path for
+// groups whose rows fit LDS (cfg 2/3 and every shard of the same shape), none/complete
+// pooling (NOPOOL) and partial pooling with the register Gibbs hand-off (SYNC_REG).
+//
+// Same work, partition and summation orders as nmc_k_run (kernels.h) -- the two are
+// bit-identical and the tests compare them -- but with ONE workgroup barrier per
+// parameter step instead of two.  nmc_k_run lets the control wave alone sum the tile
+// partials and decide (posteriorSampling.py:334-383) while the other waves wait at a
+// second barrier for the decided value; here every wave sums the partials and makes the
+// identical decision from the same LDS operands, so each wave holds the chain state it
+// needs (values, proposal scales, group log-likelihood) in registers and walks straight
+// into the next step's likelihood tiles:
+//
+//   per step k = (t, p), sp = k & 1 (every LDS hand-off double-buffered by step parity):
+//     Gibbs wave  task k-lag of the register hand-off (poll, fetch, pairwise update,
+//                 HyperParameter.update :463-498) and, when that update is the one this
+//                 step's prior needs, the step's priors -> ops[sp]
+//     control     the deferred state update of step k-1 (counters, log prior, sample and
+//                 trace rows, :369-383), both outcomes of the counters and of the tuned
+//                 scale (:385-437) -> ops[sp], priors (:293-294) -> ops[sp], the count of
+//                 the last published value, the LDS-DMA of step k+1's {z, log u}
+//     every wave proposal theta_p + scale_p * z (:304-306) from its registers and
+//                 likelihood tiles (:615-635) taken from an LDS counter -> part[sp]
+//     ---------- barrier ----------
+//     every wave the 16 tile partials in the fixed order, the group LL, the Metropolis
+//                 branches in the reference's order (:347-364); values, scale and LL
+//                 registers updated (:369-383, :608-610); the control wave publishes
+//
+// A slow wave still reading step k's operands cannot be overtaken: the next writes to
+// the same parity (step k+2) come after the barrier of step k+1, which it has not
+// reached.  The z slot of step k+2 is written during step k+1, after every wave has read
+// step k's z and log u (at the start of step k, before the barrier of step k).
+#pragma once
+#include "kernels.h"
+
+// LDS carve of nmc_k_step, in columns of 64 doubles (one per lane); the host computes
+// the same (ctx.h).
+struct nmc_step_layout {
+  int part;   // [2][NACC][NSLOT]  tile partial sums by step parity (unused slots: -0.0)
+  int st;     // [5][P]            control wave: (unused), log prior, n acc, n rej, total acc
+  int cw;     // [5]               control wave: counter outcomes of the pending step
+  int hyp;    // [6][P]            hyper state (NMC_HY_*), partial pooling
+  int zl;     // [2][2]            {z, log u} by step parity (LDS-DMA)
+  int ops;    // [2][4]            decision operands by step parity (NMC_OP_*)
+  int flag;   // [1]               wait flag, Gibbs verdict, tile counters
+  int rows;   // [nmax][NF]        the group's rows, staged once per launch
+  int total;
+};
+__host__ __device__ inline nmc_step_layout nmc_step_lds(int nacc, int P, int partial,
+                                                        int row_doubles) {
+  nmc_step_layout L;
+  L.part = 0;
+  L.st = L.part + 2 * nacc * NMC_NSLOT;
+  L.cw = L.st + 5 * P;
+  L.hyp = L.cw + 5;
+  L.zl = L.hyp + (partial ? 6 * P : 0);
+  L.ops = L.zl + 4;
+  L.flag = L.ops + 8;
+  L.rows = L.flag + 1;
+  // (+1 column: the pipelined row loops prefetch one block past a tile's rows)
+  L.total = L.rows + (row_doubles > 0 ? (row_doubles + 63) / 64 + 1 : 0);
+  return L;
+}
+// decision operands of a step: priors of the current value and of the proposal, the
+// proposal scale after an accept / a reject (tuned when due)
+enum { NMC_OP_LPC = 0, NMC_OP_LPP, NMC_OP_SA, NMC_OP_SR };
+enum { NMC_CWS_NAA = 0, NMC_CWS_NRA, NMC_CWS_NAR, NMC_CWS_NRR, NMC_CWS_TA };
+
+// The likelihood tiles of one step, taken from the step's LDS counter until none is
+// left; tile k's partial sums -> part[j * NSLOT + k] (this lane's column).  The next
+// tile is requested before the current one is computed (the atomic's return rides
+// under the tile's row reads).
+template <class Fam>
+__device__ __forceinline__ void nmc_step_tiles(const Dev& d, const Fam& fam,
+                                               const typename Fam::Reg& reg,
+                                               const typename Fam::Reg& preg,
+                                               const double* lrows, const nmc_tiling& TI,
+                                               unsigned* tc, double* part) {
+  const int lane = threadIdx.x & 63;
+  auto grab = [&]() -> unsigned {
+    unsigned k = 0;
+    if (lane == 0) k = __hip_atomic_fetch_add(tc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return k;
+  };
+  int k = (int)__builtin_amdgcn_readlane(grab(), 0);
+  while (k < TI.nt) {
+    const unsigned kn = grab();
+    const int ra = TI.start(k);
+    const int rn = TI.len(k);
+    double acc[Fam::NACC];
+    bool done = false;
+    if constexpr (nmc_paired_rows_ok<Fam>()) if (d.paired) {
+      nmc_ll_rows_lds<Fam, true>(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc, &preg);
+      done = true;
+    }
+    if (!done) nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
+#pragma unroll
+    for (int j = 0; j < Fam::NACC; ++j) part[(j * NMC_NSLOT + k) * 64] = acc[j];
+    k = (int)__builtin_amdgcn_readlane(kn, 0);
+  }
+}
+
+template <class Fam, int MODE>
+__global__ void __launch_bounds__(512)
+nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int flags) {
+  static_assert(MODE == NMC_MODE_NOPOOL || MODE == NMC_MODE_SYNC_REG,
+                "nmc_k_step: none/complete pooling or the register Gibbs hand-off");
+  constexpr bool PARTIAL = MODE == NMC_MODE_SYNC_REG;
+  constexpr int MP = Fam::MAXP;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  (void)flags;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int W = blockDim.x >> 6;
+  const int P = d.P, G = d.G, C = d.C;
+  const int g = blockIdx.x % G, cb = blockIdx.x / G;
+  const int c = nmc_lane_chain(d, cb, lane);
+  const bool live = nmc_lane_owns(d, c, lane);
+  const bool g0w = g == 0;                 // writes (and records) the chain block's hyper state
+  const int cc = c < C ? c : C - 1;
+  const int ngrp = (int)(d.off[g + 1] - d.off[g]);
+  const nmc_tiling TI = nmc_tiles(ngrp, d.tile);
+  const nmc_step_layout L = nmc_step_lds(Fam::NACC, P, PARTIAL, d.nmax * Fam::NFIELDS);
+  const size_t PGC = (size_t)P * G * C;
+  const size_t gc = (size_t)g * C + cc;
+  const bool ctl = w == 0;
+  const bool gw = PARTIAL && w == 1;       // the Gibbs wave (host: W >= 3)
+  const int lag = P >= 2 ? 2 : 1;          // Gibbs task of step gs: gs - lag
+  double* st = lds + L.st * 64 + lane;     // st[(k * P + p) * 64]
+  double* cw = lds + L.cw * 64 + lane;
+  double* hy = lds + L.hyp * 64 + lane;
+  double* ops = lds + L.ops * 64 + lane;   // ops[(sp * 4 + j) * 64]
+  double* zl = lds + L.zl * 64;            // zl[(2 * sp) * 64 + 2 * lane + {0, 1}]
+  unsigned* tcnt = (unsigned*)(lds + L.flag * 64 + 4);   // tile counters by step parity
+  double* lrows = lds + L.rows * 64;
+
+  // ---- prologue: registers (every wave), control state and hyper state (LDS) ----
+  const double* vin = ((i0 - 1) & 1) ? d.vb1 : d.vb0;
+  double th[MP], sc[MP];
+#pragma unroll
+  for (int q = 0; q < MP; ++q) {
+    th[q] = q < P ? vin[(size_t)q * G * C + gc] : 0.0;
+    sc[q] = q < P ? d.scale[(size_t)q * G * C + gc] : 0.0;
+  }
+  double LL = d.ll[gc];
+  const double gcst = fam.gconst((long)ngrp);
+  auto zl_src = [&](int tn, int pn) -> const double* {
+    return d.vzl + ((size_t)(tn - d.vbase) * PGC + (size_t)pn * G * C + gc) * 2;
+  };
+  if (ctl) {
+    for (int p = 0; p < P; ++p) {
+      const size_t ip = (size_t)p * G * C + gc;
+      st[(NMC_ST_LP * P + p) * 64] = d.lp[ip];
+      st[(NMC_ST_NA * P + p) * 64] = (double)d.nacc[ip];
+      st[(NMC_ST_NR * P + p) * 64] = (double)d.nrej[ip];
+      st[(NMC_ST_TA * P + p) * 64] = (double)d.tacc[ip];
+      if (PARTIAL) {   // hyper-parameters after iteration i0-1 (slot (i0-1) & 1)
+        const size_t ho = nmc_hslot(d, i0 - 1) + (size_t)p * C + cc;
+        const double s2 = d.s2[ho];
+        hy[(NMC_HY_MU * P + p) * 64] = d.mu[ho];
+        hy[(NMC_HY_SD * P + p) * 64] = d.hsd[ho];
+        hy[(NMC_HY_LSD * P + p) * 64] = d.hlsd[ho];
+        hy[(NMC_HY_S2 * P + p) * 64] = s2;
+        hy[(NMC_HY_SDM * P + p) * 64] = sqrt(s2 / G);
+        hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / d.hsd[ho];
+      }
+    }
+    nmc_dma16(zl_src(i0, 0), zl + (2 * ((i0 * P) & 1)) * 64);
+    for (int s = 0; s < 2; ++s)   // x + (-0.0) == x: the fixed slot sum
+      for (int j = 0; j < Fam::NACC; ++j)
+        for (int k = TI.nt; k < NMC_NSLOT; ++k)
+          lds[(L.part + (s * Fam::NACC + j) * NMC_NSLOT + k) * 64 + lane] = -0.0;
+    lds[L.flag * 64 + lane] = 0.0;   // (also zeroes both tile counters)
+    nmc_drain_vm();
+  }
+  {   // this group's rows -> LDS, once for the whole launch
+    const double* grows = obs + d.off[g] * Fam::NFIELDS;
+    const int nd = ngrp * Fam::NFIELDS;
+    for (int i = threadIdx.x; i < nd; i += blockDim.x) lrows[i] = grows[i];
+  }
+  __syncthreads();
+
+  bool ok = true;
+  int pub_p = -1;                    // control wave: published value awaiting its count
+  int pend_p = -1, pend_t = 0;       // control wave: decided step whose bookkeeping waits
+  bool q_acc = false;
+  double q_plp = 0, q_pll = 0, q_val = 0;
+  // control wave: the rest of a decided step's update (:369-383): counters, log prior,
+  // sample and trace rows
+  auto apply_pending = [&]() {
+    const int q = pend_p, tq = pend_t;
+    st[(NMC_ST_LP * P + q) * 64] = q_plp;
+    st[(NMC_ST_NA * P + q) * 64] = cw[(q_acc ? NMC_CWS_NAA : NMC_CWS_NAR) * 64];
+    st[(NMC_ST_NR * P + q) * 64] = cw[(q_acc ? NMC_CWS_NRA : NMC_CWS_NRR) * 64];
+    st[(NMC_ST_TA * P + q) * 64] = cw[NMC_CWS_TA * 64] + (q_acc ? 1.0 : 0.0);
+    if (live) {
+      const int row = nmc_record_row(d, tq);
+      if (row >= 0) {
+        const int col = q * (G + (PARTIAL ? 2 : 0)) + (PARTIAL ? 2 : 0) + g;
+        d.samples[((size_t)row * d.cols + col) * C + c] = q_val;
+      }
+      if (tq < d.trace_n) {
+        const size_t it = (((size_t)tq * P + q) * G + g) * C + c;
+        d.tflag[it] = q_acc ? 1 : 0;
+        d.tllp[it] = q_pll;
+      }
+    }
+    pend_p = -1;
+  };
+  auto count_published = [&]() {
+    if (pub_p >= 0) {
+      nmc_drain_vm();
+      if (lane == 0)
+        __hip_atomic_fetch_add(nmc_counter(d, cb, pub_p, g & 7), 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      pub_p = -1;
+    }
+  };
+  auto sel = [](const double (&a)[MP], int p) {
+    double v = a[0];
+#pragma unroll
+    for (int q = 1; q < MP; ++q)
+      if (q == p) v = a[q];
+    return v;
+  };
+
+  const int gs0 = i0 * P;
+  for (int t = i0; t < i1 && ok; ++t) {
+    NMC_STAMP(t, 0);
+    const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
+    for (int p = 0; p < P; ++p) {
+      const int gs = t * P + p, sp = gs & 1;
+      double* opk = ops + sp * 4 * 64;
+      const double* zk = zl + (2 * sp) * 64 + 2 * lane;
+      const bool due = PARTIAL && gs - lag >= gs0;   // the Gibbs wave's task gs - lag
+      const bool post_prior = due && P <= 2;         // ... is the update this step's prior needs
+      const double thp_p = sel(th, p), scp = sel(sc, p);
+
+      // ---- Gibbs wave: task gs - lag = (kt, kq), and this step's priors when due ----
+      if constexpr (PARTIAL) if (gw && due) {
+        if (W > 1 && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
+        const int k = gs - lag, kq = k % P, kt = k / P;
+        const bool r = nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1));
+        if (lane == 0)
+          __hip_atomic_store(lds + L.flag * 64 + 1, r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (r) {
+          // keep the payload loads below the poll (no instruction: wavefront scope)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          nmc_hyper_update_reg(d, cb, kt, kq, cc, lds, L.hyp, g0w);
+          if (post_prior) {
+            const double prop = thp_p + (1.0 * scp) * zk[0];
+            const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
+            const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
+            opk[NMC_OP_LPC * 64] =
+                t > 0 ? nmc_norm_logpdf_r(thp_p, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
+            opk[NMC_OP_LPP * 64] = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
+          }
+        }
+        if (W > 1) __builtin_amdgcn_s_setprio(0);
+      }
+      // ---- control wave: bookkeeping of step gs-1, operands of this step, next z ----
+      if (ctl) {
+        if (W > 1 && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
+        if (pend_p >= 0) apply_pending();
+        {
+          const double na = st[(NMC_ST_NA * P + p) * 64], nr = st[(NMC_ST_NR * P + p) * 64];
+          double naA = na + 1.0, nrA = nr, naR = na, nrR = nr + 1.0;
+          double sA = scp, sR = scp;
+          if (tune) {
+            nmc_tune(sA, naA, nrA);
+            nmc_tune(sR, naR, nrR);
+          }
+          cw[NMC_CWS_NAA * 64] = naA;
+          cw[NMC_CWS_NRA * 64] = nrA;
+          cw[NMC_CWS_NAR * 64] = naR;
+          cw[NMC_CWS_NRR * 64] = nrR;
+          cw[NMC_CWS_TA * 64] = st[(NMC_ST_TA * P + p) * 64];
+          opk[NMC_OP_SA * 64] = sA;
+          opk[NMC_OP_SR * 64] = sR;
+        }
+        if (!post_prior) {   // priors (:293-294)
+          const double prop = thp_p + (1.0 * scp) * zk[0];
+          double lpc, lpp;
+          if constexpr (PARTIAL) {
+            const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
+            const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
+            lpc = t > 0 ? nmc_norm_logpdf_r(thp_p, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
+            lpp = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
+          } else {
+            lpc = st[(NMC_ST_LP * P + p) * 64];
+            lpp = nmc_prior_logpdf(d.pfam[p], d.ppar + 8 * p, prop);
+          }
+          opk[NMC_OP_LPC * 64] = lpc;
+          opk[NMC_OP_LPP * 64] = lpp;
+        }
+        // the previous step's published value has had the work above to drain
+        if constexpr (PARTIAL) count_published();
+        const int tn = p + 1 < P ? t : t + 1;
+        const int pn = p + 1 < P ? p + 1 : 0;
+        if (tn < i1) nmc_dma16(zl_src(tn, pn), zl + (2 * (sp ^ 1)) * 64);
+        if (W > 1) __builtin_amdgcn_s_setprio(0);
+      }
+
+      // ---- every wave: the proposal and its likelihood tiles ----
+      const double lu = zk[1];
+      const double prop = thp_p + (1.0 * scp) * zk[0];   // Parameter.propose (:304-306)
+      double thp[MP];
+#pragma unroll
+      for (int q = 0; q < MP; ++q) thp[q] = q == p ? prop : th[q];
+      const typename Fam::Reg reg = fam.prepare(thp);
+      typename Fam::Reg preg = reg;   // paired rows: the partner lane's (lane ^ 32) proposal
+      if constexpr (nmc_paired_rows_ok<Fam>()) if (d.paired) {
+        const bool hi = lane >= 32;
+        double pth[MP];
+#pragma unroll
+        for (int q = 0; q < MP; ++q) {
+          const nmc_pair2 e = nmc_halves(thp[q]);
+          pth[q] = hi ? e.lo : e.hi;
+        }
+        preg = fam.prepare(pth);
+      }
+      nmc_step_tiles(d, fam, reg, preg, lrows, TI, tcnt + sp,
+                     lds + (L.part + sp * Fam::NACC * NMC_NSLOT) * 64 + lane);
+      NMC_STAMP(t, 1 + 3 * (p & 1));
+      if (ctl) nmc_drain_vm();   // the next step's {z, log u} have landed
+      __syncthreads();
+      NMC_STAMP(t, 2 + 3 * (p & 1));
+
+      // ---- every wave: group log-likelihood and the Metropolis decision (:334-383) ----
+      if (ctl && lane == 0) tcnt[sp] = 0u;   // all of this step's tiles are taken; reused at +2
+      double acc[Fam::NACC];
+#pragma unroll
+      for (int j = 0; j < Fam::NACC; ++j)
+        acc[j] = nmc_sum_slots(lds + (L.part + (sp * Fam::NACC + j) * NMC_NSLOT) * 64 + lane);
+      const double verdict = due ? lds[L.flag * 64 + 1] : 0.0;
+      const double lpc = opk[NMC_OP_LPC * 64], lpp = opk[NMC_OP_LPP * 64];
+      const double sA = opk[NMC_OP_SA * 64], sR = opk[NMC_OP_SR * 64];
+      const double llp = fam.finish_fast(reg, acc, (long)ngrp, gcst);
+      const double postp = lpp + llp;
+      const double post = lpc + LL;
+      const double diff = postp - post;
+      bool accept;
+      if (!isfinite(post) && isfinite(postp)) accept = true;        // :347-352
+      else if (!isfinite(llp)) accept = false;                      // :354-356
+      else if (!isfinite(diff)) accept = false;                     // :358-360
+      else accept = lu < diff;                                      // :362-364
+      const double vn = accept ? prop : thp_p;
+#pragma unroll
+      for (int q = 0; q < MP; ++q)
+        if (q == p) {
+          th[q] = vn;
+          sc[q] = accept ? sA : sR;
+        }
+      if (accept) LL = llp;                                         // :608-610
+      if (ctl) {
+        if constexpr (PARTIAL) {   // publish write-through; counted at the next step
+          if (live)
+            __hip_atomic_store(((t & 1) ? d.vb1 : d.vb0) + (size_t)p * G * C + gc, vn,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          pub_p = p;
+        }
+        q_acc = accept;
+        q_plp = accept ? lpp : lpc;
+        q_pll = llp;
+        q_val = vn;
+        pend_p = p;
+        pend_t = t;
+      }
+      if (p == 0) NMC_STAMP(t, 3);
+      if (due) {
+        ok = verdict == 2.0 * ((double)gs + 1);
+        if (!ok) break;
+      }
+    }
+  }
+
+  if (ctl) {
+    if constexpr (PARTIAL) count_published();   // the last parameter's count
+    if (pend_p >= 0) apply_pending();
+  }
+  // ---- epilogue: state back to HBM (control wave) ----
+  if (ctl && live && ok) {
+    double* vo = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
+#pragma unroll
+    for (int q = 0; q < MP; ++q) {
+      if (q >= P) break;
+      const size_t ip = (size_t)q * G * C + gc;
+      if (!PARTIAL) vo[ip] = th[q];   // (partial: published write-through)
+      d.lp[ip] = st[(NMC_ST_LP * P + q) * 64];
+      d.scale[ip] = sc[q];
+      d.nacc[ip] = (int)st[(NMC_ST_NA * P + q) * 64];
+      d.nrej[ip] = (int)st[(NMC_ST_NR * P + q) * 64];
+      d.tacc[ip] = (long long)st[(NMC_ST_TA * P + q) * 64];
+    }
+    d.ll[gc] = LL;
+  }
+  // ---- closing Gibbs updates, tasks ge-lag .. ge-1 (group-0 workgroups write and record
+  //      them), once every workgroup of the chain block has published its last value ----
+  if constexpr (PARTIAL) if (ok && g0w) {
+    const int ge = i1 * P;
+    if (nmc_wait_published_col(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L.flag) &&
+        gw) {
+      for (int k = ge - lag > gs0 ? ge - lag : gs0; k < ge; ++k)
+        nmc_hyper_update_reg(d, cb, k / P, k % P, cc, lds, L.hyp, true);
+    }
+  }
+  nmc_drain_vm();
+}

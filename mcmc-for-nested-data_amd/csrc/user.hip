@@ -23,17 +23,22 @@
 namespace {
 
 // kernel table entries, in name-expression order
-// (step kernel: mode m with rows in LDS at UK_RUN0 + m, rows staged at UK_RUN0 + 5 + m)
+// (nmc_k_run: mode m with rows in LDS at UK_RUN0 + m, rows staged at UK_RUN0 + 5 + m;
+// nmc_k_step: NOPOOL / SYNC_REG at UK_STEP0 / UK_STEP0 + 1)
 enum { UK_RUN0 = 0, UK_NRUN = 5, UK_GROUP_LL = 10, UK_OBS_LL_ROWS = 11, UK_OBS_LL = 12,
-       UK_N = 13 };
+       UK_STEP0 = 13, UK_GROUP_LL_RL = 15, UK_GROUP_FIN = 16, UK_N = 17 };
 const char* const kNames[UK_N] = {
     "nmc_k_run<FamUser, 0, true>", "nmc_k_run<FamUser, 1, true>", "nmc_k_run<FamUser, 2, true>",
     "nmc_k_run<FamUser, 3, true>", "nmc_k_run<FamUser, 4, true>",
     "nmc_k_run<FamUser, 0, false>", "nmc_k_run<FamUser, 1, false>",
     "nmc_k_run<FamUser, 2, false>", "nmc_k_run<FamUser, 3, false>",
-    "nmc_k_run<FamUser, 4, false>", "nmc_k_group_ll<FamUser>", "nmc_k_obs_ll_rows<FamUser>",
-    "nmc_k_obs_ll<FamUser>"};
-int run_index(const nmc_ctx* x, int mode) { return UK_RUN0 + mode + (x->d.rows_lds ? 0 : UK_NRUN); }
+    "nmc_k_run<FamUser, 4, false>", "nmc_k_group_part<FamUser, false>", "nmc_k_obs_ll_rows<FamUser>",
+    "nmc_k_obs_ll<FamUser>", "nmc_k_step<FamUser, 0>", "nmc_k_step<FamUser, 4>",
+    "nmc_k_group_part<FamUser, true>", "nmc_k_group_fin<FamUser>"};
+int run_index(const nmc_ctx* x, int mode) {
+  if (uses_step(x, mode)) return UK_STEP0 + (mode == NMC_MODE_NOPOOL ? 0 : 1);
+  return UK_RUN0 + mode + (x->d.rows_lds ? 0 : UK_NRUN);
+}
 
 struct UserKernels {   // one device's modules, loaded on first use
   hipModule_t mod[UK_N] = {};
@@ -180,7 +185,7 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
                                                    dim3 block, size_t lds) {
         if (rc) return;
         if (mode < 0 || mode >= UK_NRUN) {
-          rc = nmc_fail(-1, "user family: the pair kernel is not compiled for user families");
+          rc = nmc_fail(-1, "user family: unknown step-kernel mode");
           return;
         }
         Dev dd = d;
@@ -196,10 +201,8 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
         c.result = atoi(e) != 0;
         return 0;
       }
-      const int mode = x->d.hreg ? NMC_MODE_SYNC_REG
-                                 : x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
       int nb = 0;
-      if (int rc = user_fn(x, run_index(x, mode), &f)) return rc;
+      if (int rc = user_fn(x, run_index(x, nmc_persist_mode(x)), &f)) return rc;
       if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * x->d.W,
                                                             nmc_persist_lds(x)) != hipSuccess) {
         c.result = 0;
@@ -216,18 +219,20 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
       c.result = nmc_safe_blocks(x, nb) * x->ncu;
       return 0;
     }
-    case NMC_OP_GROUP_LL: {
+    case NMC_OP_GROUP_LL: {   // (fam_ops.h: member partials into c.aux, then the combine)
       Dev dd = d0;
       const double* obs = d0.obs;
       const double* in = c.in;
+      double* aux = c.aux;
       double* out = c.out;
-      void* args[] = {&dd, &fam, (void*)&obs, (void*)&in, &out};
-      const size_t lds = (size_t)x->d.W * 64 * sizeof(double);
-      if (int rc = user_fn(x, UK_GROUP_LL, &f)) return rc;
-      if (int rc = launch(x, f, dim3(x->d.CB * x->G), dim3(64 * x->d.W), lds,
-                          args))
+      void* a1[] = {&dd, &fam, (void*)&obs, (void*)&in, (void*)&aux};
+      if (int rc = user_fn(x, d0.rows_lds ? UK_GROUP_LL_RL : UK_GROUP_LL, &f)) return rc;
+      if (int rc = launch(x, f, dim3(d0.CB * d0.G * d0.S), dim3(64 * d0.W), nmc_group_ll_lds(x), a1))
         return rc;
-      return 0;
+      const size_t n = (size_t)d0.G * d0.C;
+      void* a2[] = {&dd, &fam, (void*)&in, (void*)&aux, (void*)&out};
+      if (int rc = user_fn(x, UK_GROUP_FIN, &f)) return rc;
+      return launch(x, f, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, a2);
     }
     case NMC_OP_OBS_LL_ROWS: {
       const int n = c.i1 - c.i0;

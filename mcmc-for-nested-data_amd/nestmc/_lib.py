@@ -64,6 +64,7 @@ SIGNATURES = {
     "nmc_set_launch_iters": (ctypes.c_int, [_vp, ctypes.c_int]),
     "nmc_get_kernel_timing": (ctypes.c_int, [_vp, _c_double_p, _c_int64_p, _c_int64_p,
                                              _c_double_p, _c_int64_p]),
+    "nmc_kernel_name": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int]),
     "nmc_split_config": (ctypes.c_int, [_vp, _c_int_p, _c_int_p]),
     "nmc_variogram": (ctypes.c_int, [ctypes.c_int, _c_double_p, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, _c_double_p]),

@@ -218,6 +218,9 @@ class Engine:
                                          ctypes.byref(pe), ctypes.byref(cl), ctypes.byref(md)))
         sm, sb = ctypes.c_int(), ctypes.c_int()
         check(self.lib.nmc_split_config(self.h, ctypes.byref(sm), ctypes.byref(sb)))
+        buf = ctypes.create_string_buffer(160)
+        check(self.lib.nmc_kernel_name(self.h, buf, len(buf)))
         return dict(waves_per_group=w.value, chain_blocks=cb.value, persistent=bool(pe.value),
                     chains_per_block=cl.value, mode=MODE_NAMES.get(md.value, str(md.value)),
-                    split_members=sm.value, chain_blocks_per_launch=sb.value)
+                    split_members=sm.value, chain_blocks_per_launch=sb.value,
+                    kernel=buf.value.decode())

@@ -17,6 +17,7 @@ family (nestmc.families) or a missing GPU/library raises.
 
 import datetime
 import os
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy
 
@@ -76,8 +77,16 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
     start_time = datetime.datetime.now()
     if not is_family(logLikelihoodFunction):
         raise TypeError(
-            "logLikelihoodFunction must be a nestmc device family (nestmc.LinearRegression, "
-            "GaussianMean, Logistic): an arbitrary Python callable cannot run on the GPU")
+            "logLikelihoodFunction must be a nestmc device family: a built-in one "
+            "(nestmc.LinearRegression, GaussianMean, Logistic) or "
+            "nestmc.DeviceLikelihood(obs_rows, source, n_params, consts=...) wrapping a "
+            "per-observation '__device__ double nmc_user_loglik(theta, row, k)' that is "
+            "compiled for the GPU at run time. A plain Python callable -- e.g. the "
+            "reference examples' functools.partial(computeLogLikelihood, data=data) "
+            "(example/regression.py:53-67, 91) -- cannot run on the GPU, and this sampler "
+            "has no CPU fallback by design; pass the callable as "
+            "DeviceLikelihood(..., host_function=callable) to keep it for host-side checks "
+            "(INTEGRATION.md, 'Porting a likelihood callable').")
     if pooling not in ("partial", "none", "complete"):
         raise Exception("Invalid pooling: ", pooling)
     names = tuple(parameterName)
@@ -139,25 +148,38 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
             chain_logs.append(lg)
     # ---- shard contiguous blocks of chains over the devices; every device
     #      initialises its own chains, their likelihoods evaluated in batches on it --
-    engines = []
-    for r, dev in enumerate(devices):
+    def make_engine(r, dev):
         s0, cnt = shard(len(chain_ids), len(devices), r)
         if cnt == 0:
-            continue
+            return None
         ids = chain_ids[s0:s0 + cnt]
         if ids != list(range(ids[0], ids[0] + cnt)):
             raise ValueError("chains must be contiguous global ids per device")
         eng = Engine(logLikelihoodFunction, sizes, cnt, pooling, priors, seed=seed,
                      chain_base=ids[0], device=dev, rng=rng)
-        sl = slice(s0, s0 + cnt)
-        st = init_chains(logLikelihoodFunction, sizes, names, ids, pooling, start_priors,
-                         startingPointValueRange, startWithMLE, threads=threads,
-                         group_ll=eng.eval_group_ll)
-        eng.set_state(st["value"], st["log_prior"], st["ll"], st["mu"], st["s2"])
-        if replay is not None:
-            eng.set_replay(*(numpy.asarray(replay[k])[sl] for k in ("z", "u", "hz", "hu")))
-        eng.set_schedule(nIter, burn, thin, 100)
-        engines.append((eng, s0, ids))
+        try:
+            sl = slice(s0, s0 + cnt)
+            st = init_chains(logLikelihoodFunction, sizes, names, ids, pooling, start_priors,
+                             startingPointValueRange, startWithMLE,
+                             threads=max(1, threads // len(devices)),
+                             group_ll=eng.eval_group_ll)
+            eng.set_state(st["value"], st["log_prior"], st["ll"], st["mu"], st["s2"])
+            if replay is not None:
+                eng.set_replay(*(numpy.asarray(replay[k])[sl] for k in ("z", "u", "hz", "hu")))
+            eng.set_schedule(nIter, burn, thin, 100)
+        except BaseException:
+            eng.close()
+            raise
+        return (eng, s0, ids)
+
+    # one host thread per engine: each initialises its chains (reference RNG order) with
+    # their likelihoods batched on its own device, concurrently with the others
+    if len(devices) > 1:
+        with ThreadPoolExecutor(max_workers=len(devices)) as ex:
+            made = list(ex.map(lambda a: make_engine(*a), enumerate(devices)))
+    else:
+        made = [make_engine(0, devices[0])]
+    engines = [e for e in made if e is not None]
 
     # ---- the device loop ----------------------------------------------------
     rec = record_iterations(nIter, burn, thin)

@@ -71,6 +71,44 @@ def test_user_poisson_matches_oracle(gpu_lib, pooling, C, G, N, n_iter):
     assert acc.mean() > 0.02
 
 
+@pytest.mark.parametrize("G,S,mode", [(64, 4, "NMC_MODE_SYNC_REG"), (128, 2, "NMC_MODE_SYNC_LDS")])
+def test_cfg5_user_logistic8_staged_rows(gpu_lib, G, S, mode):
+    """BASELINE cfg 5 as stated: a USER-supplied 8-parameter logistic, 5000 rows per group,
+    partial pooling, at group counts where each row-split member's chunk (G = 64: S = 4
+    members of 1250 rows; G = 128, the cfg-5 shard: S = 2 of 2500 rows; 64 B per row)
+    exceeds the LDS row area, so the staged-row instances nmc_k_run<FamUser, m, false> of
+    both Gibbs modes run.  Bit-identical to the built-in Logistic on every chain
+    (persistent and launch per iteration); chains 0 and 63 against the oracle."""
+    from gpu_cases import partial_state
+    from nestmc import data
+    from nestmc.families import Logistic
+    N, n_iter, seed, C = 5000, 4, 5, 64
+    X, yl, _ = data.logistic(G, N, n_coef=8, seed=1)
+    fam = Logistic(X, yl)
+    assert fam.n_params == 8 and fam.n_fields == 8
+    user = DeviceLikelihood(fam.obs(), user_models.LOGISTIC8, 8, host_function=fam)
+    sizes = [N] * G
+    st, nested = partial_state(fam, sizes, C, 8, spread=0.1)
+    a = run_engine(fam, sizes, st, numpy.arange(C), 100, n_iter, seed, tune_interval=2)
+    b = run_engine(user, sizes, st, numpy.arange(C), 100, n_iter, seed, tune_interval=2)
+    cfg = b[3]
+    assert cfg["split_members"] == S and cfg["persistent"], cfg
+    assert cfg["kernel"] == "nmc_k_run<FamUser, %s, false>" % mode, cfg
+    lau = run_engine(user, sizes, st, numpy.arange(C), 100, n_iter, seed, tune_interval=2,
+                     env={"NMC_PERSIST": "0"})
+    for k in range(3):
+        assert numpy.array_equal(a[k], b[k], equal_nan=True), k
+        assert numpy.array_equal(b[k], lau[k], equal_nan=True), k
+    sel = numpy.array([0, 63])
+    oacc, ollp, orows, margin = run_oracle(nested, st, sel, sel + 100, n_iter, seed,
+                                           tune_interval=2)
+    bad = numpy.argwhere(b[0][sel].astype(bool) != oacc)
+    assert bad.size == 0, "flag mismatch at %s (min margin %g)" % (bad[:5], margin)
+    assert close(b[1][sel], ollp, rtol=1e-10)
+    assert close(b[2][sel], orows)
+    assert b[0].mean() > 0.02
+
+
 def test_user_family_through_sample_posterior(gpu_lib, tmp_path):
     import posteriorSampling
     fam, sizes, _, _, _ = synthetic("logistic_partial", 4, 6, 25)

@@ -3,18 +3,23 @@
 import numpy
 import scipy.special
 
-# FamLogistic's own expression (csrc/families.h) as a user function, rows [x_1..x_3, y],
-# theta [b0, b1..b3]: eta = b0 + fma chain; ll = y eta - logaddexp(0, eta)
-LOGISTIC4 = r"""
+
+
+def logistic_source(k):
+    """FamLogistic's own expression (csrc/families.h) as a user function, rows
+    [x_1..x_k, y], theta [b0, b1..bk]: eta = b0 + fma chain; ll = y eta - logaddexp(0, eta)
+    (nmc_logaddexp0, the library's numpy.logaddexp restatement)."""
+    return r"""
 __device__ double nmc_user_loglik(const double* th, const double* row, const double* k) {
   double eta = th[0];
-  for (int j = 0; j < 3; ++j) eta = fma(row[j], th[j + 1], eta);
-  double lae;
-  if (eta == 0.0) lae = NMC_LN2;
-  else lae = eta > 0.0 ? eta + log1p(exp(-eta)) : log1p(exp(eta));
-  return row[3] * eta - lae;
+  for (int j = 0; j < %d; ++j) eta = fma(row[j], th[j + 1], eta);
+  return row[%d] * eta - nmc_logaddexp0(eta);
 }
-"""
+""" % (k, k)
+
+
+LOGISTIC4 = logistic_source(3)
+LOGISTIC8 = logistic_source(7)
 
 # A model no built-in family covers: Poisson regression with a log link and an exposure
 # constant, rows [x, y, lgamma(y + 1)] (the data-only term precomputed per row), theta
