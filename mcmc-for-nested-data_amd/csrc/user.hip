@@ -139,7 +139,7 @@ extern "C" int nmc_user_family_compile(const char* source, int n_fields, int n_p
   u->nf = n_fields;
   u->np = n_params;
   u->src = "#define NMC_USER_NF " + std::to_string(n_fields) + "\n#define NMC_USER_P " +
-           std::to_string(n_params) + "\n#include \"kernels.h\"\n#line 1 \"user\"\n" + source +
+           std::to_string(n_params) + "\n#include \"kernels.h\"\n#include \"step.h\"\n#line 1 \"user\"\n" + source +
            "\n#include \"fam_user.h\"\n";
   u->inc = std::string("-I") + include_dir;
   // the cheapest kernel now: a source error is reported here, with the compiler log
