@@ -173,12 +173,13 @@ enum {
   NMC_OP_CAN_PERSIST = 1,  // result = 1 if the persistent grid is co-resident
   NMC_OP_GROUP_LL = 2,     // in = theta [P][G][C] (device), out = [G][C] (device)
   NMC_OP_OBS_LL = 3,       // in = values [P][G][C] (device), out = [C][n_obs] (device)
-  NMC_OP_OBS_LL_ROWS = 4,  // sample rows [i0, i1) -> out = [C][i1 - i0][n_obs] (device)
+  NMC_OP_OBS_LL_ROWS = 4,  // sample rows [i0, i1), chains [c0, c0 + nc) -> out = [nc][i1 - i0][n_obs]
   NMC_OP_CAPACITY = 5      // result = resident step-kernel workgroups on the device
 };
 struct NmcCall {
   int op = 0;
   int i0 = 0, i1 = 0, flags = 0;
+  int c0 = 0, nc = 0;      // NMC_OP_OBS_LL_ROWS: chains [c0, c0 + nc) (nc = 0: every chain)
   const double* in = nullptr;
   double* out = nullptr;
   double* aux = nullptr;   // op-specific device scratch

@@ -85,10 +85,11 @@ static int nmc_fam_call(nmc_ctx* x, const Fam& fam, NmcCall& c) {
     case NMC_OP_OBS_LL_ROWS: {
       const int n = c.i1 - c.i0;
       if (n <= 0 || x->n_obs == 0) return 0;
-      const dim3 grid((unsigned)((x->n_obs + 255) / 256), (unsigned)x->C, (unsigned)n);
+      const int nc = c.nc > 0 ? c.nc : x->C;
+      const dim3 grid((unsigned)((x->n_obs + 255) / 256), (unsigned)nc, (unsigned)n);
       hipLaunchKernelGGL(nmc_k_obs_ll_rows<Fam>, grid, dim3(256), 0, x->stream, x->d, fam,
                          (const int*)x->gidx, x->n_obs,
-                         x->pooling == NMC_POOL_PARTIAL ? 2 : 0, c.i0, n, c.out);
+                         x->pooling == NMC_POOL_PARTIAL ? 2 : 0, c.i0, n, c.c0, c.out);
       HIPCHK(hipGetLastError());
       return 0;
     }

@@ -2048,16 +2048,16 @@ nmc_k_group_fin(Dev d, Fam fam, const double* theta, const double* part, double*
 }
 
 // StepMethod.logLikelihood (:656-659) at recorded rows of the device sample store:
-// out[c][r][i] = observation i's log-likelihood at the values of row row0 + r (the state
+// out[c - c0][r][i] = observation i's log-likelihood at the values of row row0 + r (the state
 // Sampler._printLogLikelihood evaluated at that recorded iteration, :890-891).  One
 // thread per (observation, chain, row), writes coalesced along the observations.
 // pc: 2 if the sample columns carry the hyper-parameters (partial pooling), else 0.
 template <class Fam>
 __global__ void __launch_bounds__(256)
 nmc_k_obs_ll_rows(Dev d, Fam fam, const int* __restrict__ gidx, int64_t n_obs, int pc, int row0,
-                  int nrows, double* __restrict__ out) {
+                  int nrows, int c0, double* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int c = blockIdx.y, r = blockIdx.z;
+  const int c = c0 + (int)blockIdx.y, r = blockIdx.z;   // (chains [c0, c0 + gridDim.y))
   if (i >= n_obs) return;
   const int g = gidx[i];
   const double* row = d.samples + (size_t)(row0 + r) * d.cols * d.C + c;
@@ -2066,7 +2066,7 @@ nmc_k_obs_ll_rows(Dev d, Fam fam, const int* __restrict__ gidx, int64_t n_obs, i
   for (int q = 0; q < Fam::MAXP; ++q)
     th[q] = q < d.P ? row[((size_t)q * (d.G + pc) + pc + g) * d.C] : 0.0;
   const typename Fam::Reg reg = fam.prepare(th);
-  out[((size_t)c * nrows + r) * n_obs + i] = fam.obs_ll(reg, d.obs + i * Fam::NFIELDS);
+  out[((size_t)blockIdx.y * nrows + r) * n_obs + i] = fam.obs_ll(reg, d.obs + i * Fam::NFIELDS);
 }
 
 // Per-observation LL at the values in `value` [P][G][C] -> out [C][n_obs].

@@ -851,9 +851,11 @@ int nmc_obs_ll_rows(nmc_ctx* x, int row_begin, int n_rows, double* out) {
 }
 
 // saveLogLikelihood (Sampler._printLogLikelihood :907-909 at every recorded row, the LL
-// of :656-659 evaluated at the recorded values): batches of rows are evaluated on the
-// device into one of two buffers and copied to pinned host memory while the host
-// formats and appends the previous batch, one thread per group of chain files.
+// of :656-659 evaluated at the recorded values): batches are evaluated on the device into
+// one of two buffers and copied to pinned host memory while the host formats and appends
+// the previous batch, one thread per group of chain files.  A batch is several rows of
+// every chain within a 256 MiB budget, or -- when one row of every chain exceeds it
+// (many chains x many observations) -- one row of a sub-range of the chains.
 int nmc_write_ll_csvs(nmc_ctx* x, const char* dir, const int32_t* chain_ids, int threads) {
   hipSetDevice(x->device);
   HIPCHK(hipStreamSynchronize(x->stream));
@@ -863,10 +865,20 @@ int nmc_write_ll_csvs(nmc_ctx* x, const char* dir, const int32_t* chain_ids, int
   const int64_t n_obs = x->n_obs;
   if (rows == 0 || n_obs == 0) return 0;
   if (int rc = ensure_gidx(x)) return rc;
-  const size_t per_row = (size_t)C * n_obs * 8;
-  int nb = (int)std::max<size_t>(1, ((size_t)256 << 20) / per_row);
-  nb = std::min(nb, std::min(rows, 65535));
-  const int nbatch = (rows + nb - 1) / nb;
+  const size_t budget = (size_t)256 << 20;
+  const size_t per_chain_row = (size_t)n_obs * 8;
+  const size_t per_row = (size_t)C * per_chain_row;
+  int nb, ncb;   // rows per batch, chains per batch
+  if (per_row <= budget) {
+    nb = (int)std::min<size_t>({budget / per_row, (size_t)rows, (size_t)65535});
+    ncb = C;
+  } else {
+    nb = 1;
+    ncb = (int)std::max<size_t>(1, std::min<size_t>(budget / per_chain_row, 65535));
+  }
+  const int nrb = (rows + nb - 1) / nb, ncbk = (C + ncb - 1) / ncb;
+  const int nbatch = nrb * ncbk;   // batch b: rows of block b / ncbk, chains of block b % ncbk
+  const size_t buf_bytes = (size_t)nb * ncb * per_chain_row;
   double* dbuf[2] = {nullptr, nullptr};
   double* hbuf[2] = {nullptr, nullptr};
   hipEvent_t ev[2] = {nullptr, nullptr};
@@ -879,41 +891,54 @@ int nmc_write_ll_csvs(nmc_ctx* x, const char* dir, const int32_t* chain_ids, int
     }
   };
   for (int i = 0; i < 2 && !rc; ++i) {
-    if (hipMalloc(&dbuf[i], nb * per_row) != hipSuccess ||
-        hipHostMalloc(&hbuf[i], nb * per_row, hipHostMallocDefault) != hipSuccess ||
+    if (hipMalloc(&dbuf[i], buf_bytes) != hipSuccess ||
+        hipHostMalloc(&hbuf[i], buf_bytes, hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
       rc = fail(-2, "write_ll_csvs: out of device or pinned host memory");
   }
+  struct Batch { int r0, n, c0, nc; };
+  auto batch = [&](int b) {
+    Batch q;
+    q.r0 = (b / ncbk) * nb;
+    q.n = std::min(nb, rows - q.r0);
+    q.c0 = (b % ncbk) * ncb;
+    q.nc = std::min(ncb, C - q.c0);
+    return q;
+  };
   auto launch = [&](int b) -> int {
-    const int r0 = b * nb, n = std::min(nb, rows - r0);
+    const Batch q = batch(b);
     NmcCall c;
     c.op = NMC_OP_OBS_LL_ROWS;
-    c.i0 = r0;
-    c.i1 = r0 + n;
+    c.i0 = q.r0;
+    c.i1 = q.r0 + q.n;
+    c.c0 = q.c0;
+    c.nc = q.nc;
     c.out = dbuf[b & 1];
     if (int e = nmc_call_family(x, c)) return e;
-    HIPCHK(hipMemcpyAsync(hbuf[b & 1], dbuf[b & 1], n * per_row, hipMemcpyDeviceToHost, x->stream));
+    HIPCHK(hipMemcpyAsync(hbuf[b & 1], dbuf[b & 1], (size_t)q.n * q.nc * per_chain_row,
+                          hipMemcpyDeviceToHost, x->stream));
     HIPCHK(hipEventRecord(ev[b & 1], x->stream));
     return 0;
   };
-  const int T = std::max(1, std::min(threads, C));
   if (!rc) rc = launch(0);
   for (int b = 0; b < nbatch && !rc; ++b) {
     if (b + 1 < nbatch && (rc = launch(b + 1))) break;
     if (hipEventSynchronize(ev[b & 1]) != hipSuccess) { rc = fail(-2, "write_ll_csvs: device"); break; }
-    const int n = std::min(nb, rows - b * nb);
+    const Batch q = batch(b);
     const double* hb = hbuf[b & 1];
+    const int T = std::max(1, std::min(threads, q.nc));
     std::vector<std::string> errs(T);
     auto work = [&](int tid) {
       std::string s;
-      for (int c = tid; c < C; c += T) {
+      for (int k = tid; k < q.nc; k += T) {
+        const int c = q.c0 + k;
         char path[4096];
         snprintf(path, sizeof(path), "%slogLikelihood.%d.csv", dir, chain_ids[c]);
-        FILE* f = fopen(path, b == 0 ? "w" : "a");
+        FILE* f = fopen(path, q.r0 == 0 ? "w" : "a");
         if (!f) { errs[tid] = std::string("cannot open ") + path; return; }
         s.clear();
-        for (int r = 0; r < n; ++r) {
-          const double* v = hb + ((size_t)c * n + r) * n_obs;
+        for (int r = 0; r < q.n; ++r) {
+          const double* v = hb + ((size_t)k * q.n + r) * n_obs;
           for (int64_t i = 0; i < n_obs; ++i) {
             if (i) s += ',';
             put_f(s, v[i]);

@@ -138,7 +138,17 @@ extern "C" int nmc_user_family_compile(const char* source, int n_fields, int n_p
   UserFamily* u = new UserFamily();
   u->nf = n_fields;
   u->np = n_params;
-  u->src = "#define NMC_USER_NF " + std::to_string(n_fields) + "\n#define NMC_USER_P " +
+  // the library's own build-time kernel constants, so the JIT kernels index LDS and tiles
+  // exactly as the host carve (nmc_lds / nmc_step_lds / nmc_tiles) computed them
+  const std::string defs = "#define NMC_NSLOT_N " + std::to_string((int)NMC_NSLOT) +
+                           "\n#define NMC_HYPER_NS " + std::to_string((int)NMC_HYPER_NS) +
+                           "\n#define NMC_LDS_ROW_DOUBLES " +
+                           std::to_string((int)NMC_LDS_ROW_DOUBLES) + "\n"
+#ifdef NMC_STAMPS
+                           "#define NMC_STAMPS 1\n"
+#endif
+      ;
+  u->src = defs + "#define NMC_USER_NF " + std::to_string(n_fields) + "\n#define NMC_USER_P " +
            std::to_string(n_params) + "\n#include \"kernels.h\"\n#include \"step.h\"\n#line 1 \"user\"\n" + source +
            "\n#include \"fam_user.h\"\n";
   u->inc = std::string("-I") + include_dir;
@@ -240,12 +250,13 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
       Dev dd = d0;
       const int* gidx = (const int*)x->gidx;
       int64_t n_obs = x->n_obs;
-      int pc = x->pooling == NMC_POOL_PARTIAL ? 2 : 0, row0 = c.i0, nrows = n;
+      int pc = x->pooling == NMC_POOL_PARTIAL ? 2 : 0, row0 = c.i0, nrows = n, c0 = c.c0;
+      const int nc = c.nc > 0 ? c.nc : x->C;
       double* out = c.out;
-      void* args[] = {&dd, &fam, (void*)&gidx, &n_obs, &pc, &row0, &nrows, &out};
+      void* args[] = {&dd, &fam, (void*)&gidx, &n_obs, &pc, &row0, &nrows, &c0, &out};
       if (int rc = user_fn(x, UK_OBS_LL_ROWS, &f)) return rc;
       return launch(x, f,
-                    dim3((unsigned)((x->n_obs + 255) / 256), (unsigned)x->C, (unsigned)n),
+                    dim3((unsigned)((x->n_obs + 255) / 256), (unsigned)nc, (unsigned)n),
                     dim3(256), 0, args);
     }
     case NMC_OP_OBS_LL: {

@@ -78,13 +78,34 @@ def test_cfg5_logistic_p8_rows_beyond_lds(gpu_lib):
     C = 64
     st, nested = partial_state(fam, sizes, C, 8, spread=0.1)
     dev = run_engine(fam, sizes, st, numpy.arange(C), 100, n_iter, seed, tune_interval=2)
-    assert dev[3]["persistent"]
-    lau = run_engine(fam, sizes, st, numpy.arange(C), 100, n_iter, seed, tune_interval=2,
+    # (S = 5 members of 1000 rows: a row split always runs persistent -- its members
+    # exchange every step -- so there is no launch-per-iteration form to compare with)
+    assert dev[3]["persistent"] and dev[3]["split_members"] == 5, dev[3]
+    sel = numpy.array([0, 63])
+    _check_vs_oracle(dev, nested, st, sel, sel + 100, n_iter, seed, tune_interval=2)
+    assert dev[0].mean() > 0.02
+
+
+def test_staged_rows_unsplit_launch_modes(gpu_lib):
+    """Rows beyond LDS WITHOUT a row split (130 groups of 1200 8-field rows: 75 KiB per
+    group, S = 1): the staged-row step kernel persistent and launched per iteration must
+    agree bit for bit; chains 0 and 63 against the oracle."""
+    G, N, n_iter, seed = 130, 1200, 5, 9
+    X, yl, _ = data.logistic(G, N, n_coef=8, seed=4)
+    fam = Logistic(X, yl)
+    sizes = [N] * G
+    C = 64
+    st, nested = partial_state(fam, sizes, C, 8, spread=0.1)
+    dev = run_engine(fam, sizes, st, numpy.arange(C), 7, n_iter, seed, tune_interval=2)
+    assert dev[3]["split_members"] == 1 and dev[3]["persistent"], dev[3]
+    assert dev[3]["kernel"].endswith(", false>"), dev[3]
+    lau = run_engine(fam, sizes, st, numpy.arange(C), 7, n_iter, seed, tune_interval=2,
                      env={"NMC_PERSIST": "0"})
+    assert not lau[3]["persistent"], lau[3]
     for k in range(3):
         assert numpy.array_equal(dev[k], lau[k], equal_nan=True), k
     sel = numpy.array([0, 63])
-    _check_vs_oracle(dev, nested, st, sel, sel + 100, n_iter, seed, tune_interval=2)
+    _check_vs_oracle(dev, nested, st, sel, sel + 7, n_iter, seed, tune_interval=2)
     assert dev[0].mean() > 0.02
 
 

@@ -71,14 +71,14 @@ def test_user_poisson_matches_oracle(gpu_lib, pooling, C, G, N, n_iter):
     assert acc.mean() > 0.02
 
 
-@pytest.mark.parametrize("G,S,mode", [(64, 4, "NMC_MODE_SYNC_REG"), (128, 2, "NMC_MODE_SYNC_LDS")])
-def test_cfg5_user_logistic8_staged_rows(gpu_lib, G, S, mode):
+@pytest.mark.parametrize("G,S", [(64, 4), (128, 2)])
+def test_cfg5_user_logistic8_staged_rows(gpu_lib, G, S):
     """BASELINE cfg 5 as stated: a USER-supplied 8-parameter logistic, 5000 rows per group,
     partial pooling, at group counts where each row-split member's chunk (G = 64: S = 4
     members of 1250 rows; G = 128, the cfg-5 shard: S = 2 of 2500 rows; 64 B per row)
-    exceeds the LDS row area, so the staged-row instances nmc_k_run<FamUser, m, false> of
-    both Gibbs modes run.  Bit-identical to the built-in Logistic on every chain
-    (persistent and launch per iteration); chains 0 and 63 against the oracle."""
+    exceeds the LDS row area, so the staged-row instances nmc_k_run<FamUser, m, false>
+    run (a row split is always persistent: its members exchange every step).  Bit-identical
+    to the built-in Logistic on every chain; chains 0 and 63 against the oracle."""
     from gpu_cases import partial_state
     from nestmc import data
     from nestmc.families import Logistic
@@ -93,12 +93,10 @@ def test_cfg5_user_logistic8_staged_rows(gpu_lib, G, S, mode):
     b = run_engine(user, sizes, st, numpy.arange(C), 100, n_iter, seed, tune_interval=2)
     cfg = b[3]
     assert cfg["split_members"] == S and cfg["persistent"], cfg
-    assert cfg["kernel"] == "nmc_k_run<FamUser, %s, false>" % mode, cfg
-    lau = run_engine(user, sizes, st, numpy.arange(C), 100, n_iter, seed, tune_interval=2,
-                     env={"NMC_PERSIST": "0"})
+    assert cfg["kernel"].startswith("nmc_k_run<FamUser, NMC_MODE_SYNC"), cfg
+    assert cfg["kernel"].endswith(", false>"), cfg   # rows staged from global memory
     for k in range(3):
         assert numpy.array_equal(a[k], b[k], equal_nan=True), k
-        assert numpy.array_equal(b[k], lau[k], equal_nan=True), k
     sel = numpy.array([0, 63])
     oacc, ollp, orows, margin = run_oracle(nested, st, sel, sel + 100, n_iter, seed,
                                            tune_interval=2)
