@@ -191,6 +191,8 @@ enum { NMC_RUN_HYPER_LOAD = 1 };
 #endif
 enum { NMC_NSLOT = NMC_NSLOT_N };
 enum { NMC_SPIN_LIMIT = 1 << 22 };
+// diagnostic stamps buffer (make stamps): 1024 phase / tile words + 4 per workgroup
+enum { NMC_STAMP_WORDS = 1024 + 4 * 4096 };
 // CU count the row split is sized for (a full MI355X), whatever the device reports
 enum { NMC_SPLIT_CU_BASIS = 256 };
 

@@ -1057,18 +1057,18 @@ int nmc_debug_prior_logpdf(int fam, const double* prm8, const double* xs, int n,
 }
 
 // Diagnostic build only: (re)allocate and zero the stamp buffer (n > 0) and/or copy
-// it back (out != NULL); [2 blocks][2 waves][8 iterations][16 slots] shader clocks.
+// it back (out != NULL): NMC_STAMP_WORDS uint64 (kernels.h, step.h for the layouts).
 int nmc_debug_stamps(nmc_ctx* x, int n, uint64_t* out) {
 #ifdef NMC_STAMPS
   hipSetDevice(x->device);
   if (n > 0) {
     if (!x->d.stamps)
-      if (int rc = dalloc(x, &x->d.stamps, 1024)) return rc;
-    HIPCHK(hipMemset(x->d.stamps, 0, 1024 * 8));
+      if (int rc = dalloc(x, &x->d.stamps, NMC_STAMP_WORDS)) return rc;
+    HIPCHK(hipMemset(x->d.stamps, 0, NMC_STAMP_WORDS * 8));
   }
-  if (out) {   // [0, 512): phase stamps; [512, 1024): tile stamps (nmc_k_run)
+  if (out) {   // layouts: kernels.h NMC_STAMP (nmc_k_run), step.h NMC_SW / NMC_ST / NMC_SL
     HIPCHK(hipStreamSynchronize(x->stream));
-    HIPCHK(hipMemcpy(out, x->d.stamps, 1024 * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out, x->d.stamps, NMC_STAMP_WORDS * 8, hipMemcpyDeviceToHost));
   }
   return 0;
 #else

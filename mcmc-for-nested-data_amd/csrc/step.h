@@ -61,6 +61,44 @@ __host__ __device__ inline nmc_step_layout nmc_step_lds(int nacc, int P, int par
   L.total = L.rows + (row_doubles > 0 ? (row_doubles + 63) / 64 + 1 : 0);
   return L;
 }
+// Diagnostic build only (make stamps, never shipped; tools/steptl.py reads them):
+//   [0, 512)      workgroup 0, wave w, launch step si < 8: ((w * 8 + si) * 8 + slot) shader
+//                 clocks; slots 0 step start, 1 role work done, 2 tiles done, 3 past the
+//                 barrier, 4 decided
+//   [512, 1024)   workgroup 0, tile k of launch step si < 8: (si * 16 + k) * 4 + {start,
+//                 end, wave}
+//   [1024, ...)   every workgroup b: 1024 + b * 4 + {entry, prologue done, loop done, exit},
+//                 s_memrealtime (100 MHz, one clock for the whole chip)
+#ifdef NMC_STAMPS
+#define NMC_SW(si, slot)                                                                  \
+  do {                                                                                    \
+    if (d.stamps && blockIdx.x == 0 && (si) >= 0 && (si) < 8 && (threadIdx.x & 63) == 0)  \
+      d.stamps[((w) * 8 + (si)) * 8 + (slot)] = __builtin_amdgcn_s_memtime();             \
+  } while (0)
+#define NMC_SL(slot)                                                                      \
+  do {                                                                                    \
+    if (d.stamps && threadIdx.x == 0)                                                     \
+      d.stamps[1024 + (size_t)blockIdx.x * 4 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#ifdef NMC_STAMPS_TILES   // (tile stamps too: -DNMC_STAMPS_TILES; with every stamp in the
+                          // linreg instance the backend fails with an illegal VGPR->SGPR copy)
+#define NMC_ST(si, k, e, wv)                                                              \
+  do {                                                                                    \
+    if (d.stamps && blockIdx.x == 0 && (si) >= 0 && (si) < 8 && (k) < 16 &&               \
+        (threadIdx.x & 63) == 0) {                                                        \
+      d.stamps[512 + ((si) * 16 + (k)) * 4 + (e)] = __builtin_amdgcn_s_memtime();         \
+      if (e) d.stamps[512 + ((si) * 16 + (k)) * 4 + 2] = (unsigned long long)(wv);        \
+    }                                                                                     \
+  } while (0)
+#else
+#define NMC_ST(si, k, e, wv) do {} while (0)
+#endif
+#else
+#define NMC_SW(si, slot) do {} while (0)
+#define NMC_SL(slot) do {} while (0)
+#define NMC_ST(si, k, e, wv) do {} while (0)
+#endif
+
 // decision operands of a step: priors of the current value and of the proposal, the
 // proposal scale after an accept / a reject (tuned when due)
 enum { NMC_OP_LPC = 0, NMC_OP_LPP, NMC_OP_SA, NMC_OP_SR };
@@ -75,8 +113,11 @@ __device__ __forceinline__ void nmc_step_tiles(const Dev& d, const Fam& fam,
                                                const typename Fam::Reg& reg,
                                                const typename Fam::Reg& preg,
                                                const double* lrows, const nmc_tiling& TI,
-                                               unsigned* tc, double* part) {
+                                               unsigned* tc, double* part, int si = 0) {
   const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  (void)si;
+  (void)w;
   auto grab = [&]() -> unsigned {
     unsigned k = 0;
     if (lane == 0) k = __hip_atomic_fetch_add(tc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -87,6 +128,7 @@ __device__ __forceinline__ void nmc_step_tiles(const Dev& d, const Fam& fam,
     const unsigned kn = grab();
     const int ra = TI.start(k);
     const int rn = TI.len(k);
+    NMC_ST(si, k, 0, w);
     double acc[Fam::NACC];
     bool done = false;
     if constexpr (nmc_paired_rows_ok<Fam>()) if (d.paired) {
@@ -96,6 +138,7 @@ __device__ __forceinline__ void nmc_step_tiles(const Dev& d, const Fam& fam,
     if (!done) nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
 #pragma unroll
     for (int j = 0; j < Fam::NACC; ++j) part[(j * NMC_NSLOT + k) * 64] = acc[j];
+    NMC_ST(si, k, 1, w);
     k = (int)__builtin_amdgcn_readlane(kn, 0);
   }
 }
@@ -134,6 +177,7 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
   unsigned* tcnt = (unsigned*)(lds + L.flag * 64 + 4);   // tile counters by step parity
   double* lrows = lds + L.rows * 64;
 
+  NMC_SL(0);
   // ---- prologue: registers (every wave), control state and hyper state (LDS) ----
   const double* vin = ((i0 - 1) & 1) ? d.vb1 : d.vb0;
   double th[MP], sc[MP];
@@ -179,6 +223,7 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
     for (int i = threadIdx.x; i < nd; i += blockDim.x) lrows[i] = grows[i];
   }
   __syncthreads();
+  NMC_SL(1);
 
   bool ok = true;
   int pub_p = -1;                    // control wave: published value awaiting its count
@@ -226,7 +271,6 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
 
   const int gs0 = i0 * P;
   for (int t = i0; t < i1 && ok; ++t) {
-    NMC_STAMP(t, 0);
     const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
     for (int p = 0; p < P; ++p) {
       const int gs = t * P + p, sp = gs & 1;
@@ -235,6 +279,8 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
       const bool due = PARTIAL && gs - lag >= gs0;   // the Gibbs wave's task gs - lag
       const bool post_prior = due && P <= 2;         // ... is the update this step's prior needs
       const double thp_p = sel(th, p), scp = sel(sc, p);
+      const int si = gs - gs0;   // (stamps)
+      NMC_SW(si, 0);
 
       // ---- Gibbs wave: task gs - lag = (kt, kq), and this step's priors when due ----
       if constexpr (PARTIAL) if (gw && due) {
@@ -303,6 +349,7 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
       }
 
       // ---- every wave: the proposal and its likelihood tiles ----
+      NMC_SW(si, 1);
       const double lu = zk[1];
       const double prop = thp_p + (1.0 * scp) * zk[0];   // Parameter.propose (:304-306)
       double thp[MP];
@@ -321,11 +368,11 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
         preg = fam.prepare(pth);
       }
       nmc_step_tiles(d, fam, reg, preg, lrows, TI, tcnt + sp,
-                     lds + (L.part + sp * Fam::NACC * NMC_NSLOT) * 64 + lane);
-      NMC_STAMP(t, 1 + 3 * (p & 1));
+                     lds + (L.part + sp * Fam::NACC * NMC_NSLOT) * 64 + lane, si);
       if (ctl) nmc_drain_vm();   // the next step's {z, log u} have landed
+      NMC_SW(si, 2);
       __syncthreads();
-      NMC_STAMP(t, 2 + 3 * (p & 1));
+      NMC_SW(si, 3);
 
       // ---- every wave: group log-likelihood and the Metropolis decision (:334-383) ----
       if (ctl && lane == 0) tcnt[sp] = 0u;   // all of this step's tiles are taken; reused at +2
@@ -367,7 +414,7 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
         pend_p = p;
         pend_t = t;
       }
-      if (p == 0) NMC_STAMP(t, 3);
+      NMC_SW(si, 4);
       if (due) {
         ok = verdict == 2.0 * ((double)gs + 1);
         if (!ok) break;
@@ -375,6 +422,7 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
     }
   }
 
+  NMC_SL(2);
   if (ctl) {
     if constexpr (PARTIAL) count_published();   // the last parameter's count
     if (pend_p >= 0) apply_pending();
@@ -406,4 +454,5 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
     }
   }
   nmc_drain_vm();
+  NMC_SL(3);
 }

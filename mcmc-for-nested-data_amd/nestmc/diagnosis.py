@@ -67,11 +67,16 @@ class Diagnostic:
                 keys = [k for k in d.columns if k not in ("chain", "index")]
                 self.partiallyPooled = any("_" in k for k in keys)
                 self.completelyPooled = not any("01]" in k for k in keys)
-            v = d[keys].to_numpy(dtype=numpy.float64).T   # [K, rows]
-            if v.shape[1] - half != half:    # the reference cannot halve an odd count (:155)
-                raise ValueError("could not broadcast input array from shape (%d,) into shape "
-                                 "(%d,)" % (v.shape[1] - half, half))
-            blocks += [v[:, :half], v[:, half:]]
+            v = d[keys].to_numpy(dtype=numpy.float64).T   # [K, rows of this file]
+            # every file is cut at the FIRST file's row count, [0:half] and [half:rows]
+            # (:136-155): a longer later file is truncated; a shorter one, or an odd first
+            # count, fails where the reference's assignment fails
+            first, second = v[:, :half], v[:, half:rows]
+            for part in (first, second):
+                if part.shape[1] != half:
+                    raise ValueError("could not broadcast input array from shape (%d,) into "
+                                     "shape (%d,)" % (part.shape[1], half))
+            blocks += [first, second]
         self._keys = keys or []
         self._m = len(blocks)
         self._n = blocks[0].shape[1] if blocks else 0

@@ -91,6 +91,33 @@ def test_odd_row_count_raises_like_reference(case, tmp_path, monkeypatch):
         _run_product(case, tmp_path, monkeypatch)
 
 
+@pytest.mark.parametrize("case", SMALL[:2])
+def test_longer_later_files_cut_like_reference(case, tmp_path, monkeypatch):
+    """The convergence diagnostic cuts every file at the FIRST file's row count
+    (sampleDiagnosis.py:136-155): an extra row appended to every later file leaves the
+    diagnostic files unchanged (the sample Summary, :382-491, reads every row, so the
+    summary and stdout are not compared here)."""
+    import glob
+    from nestmc import diagnosis
+    monkeypatch.setattr(diagnosis, "variogram", lambda x, device=0: numpy.array(
+        [[od.variogram(x[k], t) for t in range(x.shape[2])] for k in range(x.shape[0])]))
+    out = str(tmp_path / case)
+    shutil.copytree(_source(case), os.path.join(out, "sample"))
+    files = glob.glob(os.path.join(out, "sample") + "/sample*.csv")
+    assert len(files) >= 2
+    for fn in files[1:]:
+        last = open(fn).read().splitlines()[-1]
+        with open(fn, "a") as f:
+            f.write(last + "\n")
+    with contextlib.redirect_stdout(io.StringIO()):
+        diagnosis.diagnose_samples(out, True, True, 0)
+    names = [n for n in sorted(os.listdir(os.path.join(GOLD, case)))
+             if n not in ("stdout.txt", "summary.csv")]
+    assert names
+    for name in names:
+        assert open(os.path.join(out, "diagnostic", name)).read() == _gold(case, name), name
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES)
 def test_gpu_diagnose_samples_matches_reference(gpu_lib, case, tmp_path):

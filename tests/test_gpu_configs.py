@@ -87,15 +87,17 @@ def test_cfg5_logistic_p8_rows_beyond_lds(gpu_lib):
 
 
 def test_staged_rows_unsplit_launch_modes(gpu_lib):
-    """Rows beyond LDS WITHOUT a row split (130 groups of 1200 8-field rows: 75 KiB per
-    group, S = 1): the staged-row step kernel persistent and launched per iteration must
-    agree bit for bit; chains 0 and 63 against the oracle."""
-    G, N, n_iter, seed = 130, 1200, 5, 9
-    X, yl, _ = data.logistic(G, N, n_coef=8, seed=4)
+    """Rows beyond LDS WITHOUT a row split (130 groups of 1700 5-field rows: 66 KiB per
+    group, S = 1; G > 128: the multi-leaf Gibbs update): the staged-row step kernel
+    persistent and launched per iteration must agree bit for bit; chains 0 and 63
+    against the oracle."""
+    G, N, n_iter, seed = 130, 1700, 5, 9
+    X, yl, _ = data.logistic(G, N, n_coef=5, seed=4)
     fam = Logistic(X, yl)
+    assert fam.n_fields == 5 and fam.n_params == 5
     sizes = [N] * G
     C = 64
-    st, nested = partial_state(fam, sizes, C, 8, spread=0.1)
+    st, nested = partial_state(fam, sizes, C, 5, spread=0.1)
     dev = run_engine(fam, sizes, st, numpy.arange(C), 7, n_iter, seed, tune_interval=2)
     assert dev[3]["split_members"] == 1 and dev[3]["persistent"], dev[3]
     assert dev[3]["kernel"].endswith(", false>"), dev[3]
