@@ -81,10 +81,12 @@ static inline int run_mode(const nmc_ctx* x) {
 }
 
 // The one-barrier step kernel (step.h) runs mode `mode` when the groups' rows are in LDS,
-// there is no row split, and the mode is none/complete pooling or the register hand-off.
+// there is no row split, and the mode is none/complete pooling or the register hand-off of
+// at most 64 groups (one 64-value fetch per Gibbs task).
 static inline bool uses_step(const nmc_ctx* x, int mode) {
   return x->step_ok && x->d.rows_lds && x->d.S == 1 &&
-         (mode == NMC_MODE_NOPOOL || (mode == NMC_MODE_SYNC_REG && x->d.W >= 3));
+         (mode == NMC_MODE_NOPOOL ||
+          (mode == NMC_MODE_SYNC_REG && x->d.W >= 3 && x->d.G <= 64));
 }
 static inline size_t step_lds_bytes(const nmc_ctx* x) {
   return (size_t)nmc_step_lds(x->nacc, x->d.P, x->pooling == NMC_POOL_PARTIAL,

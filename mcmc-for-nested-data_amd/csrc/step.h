@@ -40,7 +40,7 @@ struct nmc_step_layout {
   int st;     // [5][P]            control wave: (unused), log prior, n acc, n rej, total acc
   int cw;     // [5]               control wave: counter outcomes of the pending step
   int hyp;    // [6][P]            hyper state (NMC_HY_*), partial pooling
-  int zl;     // [2][2]            {z, log u} by step parity (LDS-DMA)
+  int zl;     // [4][2]            {z, log u} ring by step (LDS-DMA, two steps ahead)
   int ops;    // [2][4]            decision operands by step parity (NMC_OP_*)
   int flag;   // [1]               wait flag, Gibbs verdict, tile counters
   int rows;   // [nmax][NF]        the group's rows, staged once per launch
@@ -54,7 +54,7 @@ __host__ __device__ inline nmc_step_layout nmc_step_lds(int nacc, int P, int par
   L.cw = L.st + 5 * P;
   L.hyp = L.cw + 5;
   L.zl = L.hyp + (partial ? 6 * P : 0);
-  L.ops = L.zl + 4;
+  L.ops = L.zl + 8;
   L.flag = L.ops + 8;
   L.rows = L.flag + 1;
   // (+1 column: the pipelined row loops prefetch one block past a tile's rows)
@@ -143,6 +143,19 @@ __device__ __forceinline__ void nmc_step_tiles(const Dev& d, const Fam& fam,
   }
 }
 
+// field-wise a ? x : y of a family's per-lane registers (a struct of doubles)
+template <class R>
+__device__ __forceinline__ R nmc_reg_select(bool a, const R& x, const R& y) {
+  static_assert(sizeof(R) % sizeof(double) == 0, "Fam::Reg: doubles only");
+  R r;
+  const double* px = reinterpret_cast<const double*>(&x);
+  const double* py = reinterpret_cast<const double*>(&y);
+  double* pr = reinterpret_cast<double*>(&r);
+#pragma unroll
+  for (unsigned i = 0; i < sizeof(R) / sizeof(double); ++i) pr[i] = a ? px[i] : py[i];
+  return r;
+}
+
 template <class Fam, int MODE>
 __global__ void __launch_bounds__(512)
 nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int flags) {
@@ -150,11 +163,12 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
                 "nmc_k_step: none/complete pooling or the register Gibbs hand-off");
   constexpr bool PARTIAL = MODE == NMC_MODE_SYNC_REG;
   constexpr int MP = Fam::MAXP;
+  constexpr bool PAIRED_OK = nmc_paired_rows_ok<Fam>();
+  using Reg = typename Fam::Reg;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   (void)flags;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int W = blockDim.x >> 6;
   const int P = d.P, G = d.G, C = d.C;
   const int g = blockIdx.x % G, cb = blockIdx.x / G;
   const int c = nmc_lane_chain(d, cb, lane);
@@ -167,15 +181,17 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
   const size_t PGC = (size_t)P * G * C;
   const size_t gc = (size_t)g * C + cc;
   const bool ctl = w == 0;
-  const bool gw = PARTIAL && w == 1;       // the Gibbs wave (host: W >= 3)
+  const bool gw = PARTIAL && w == 1;       // the Gibbs wave (host: W >= 3, G <= 64)
   const int lag = P >= 2 ? 2 : 1;          // Gibbs task of step gs: gs - lag
+  const bool paired = PAIRED_OK && d.paired;
   double* st = lds + L.st * 64 + lane;     // st[(k * P + p) * 64]
   double* cw = lds + L.cw * 64 + lane;
   double* hy = lds + L.hyp * 64 + lane;
   double* ops = lds + L.ops * 64 + lane;   // ops[(sp * 4 + j) * 64]
-  double* zl = lds + L.zl * 64;            // zl[(2 * sp) * 64 + 2 * lane + {0, 1}]
+  double* zl = lds + L.zl * 64;            // {z, log u} of step gs: zl + (2 * (gs & 3)) * 64
   unsigned* tcnt = (unsigned*)(lds + L.flag * 64 + 4);   // tile counters by step parity
   double* lrows = lds + L.rows * 64;
+  const int gs0 = i0 * P, ge = i1 * P;
 
   NMC_SL(0);
   // ---- prologue: registers (every wave), control state and hyper state (LDS) ----
@@ -188,8 +204,12 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
   }
   double LL = d.ll[gc];
   const double gcst = fam.gconst((long)ngrp);
-  auto zl_src = [&](int tn, int pn) -> const double* {
-    return d.vzl + ((size_t)(tn - d.vbase) * PGC + (size_t)pn * G * C + gc) * 2;
+  // {z, log u} of global step k -> its ring slot (k & 3), by LDS-DMA: issued two steps ahead
+  // by the control wave, landed (its vmcnt drain) before the barrier of the step before
+  auto put_zl = [&](int k) {
+    if (k < ge)
+      nmc_dma16(d.vzl + ((size_t)(k / P - d.vbase) * PGC + (size_t)(k % P) * G * C + gc) * 2,
+                zl + (2 * (k & 3)) * 64);
   };
   if (ctl) {
     for (int p = 0; p < P; ++p) {
@@ -209,7 +229,8 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
         hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / d.hsd[ho];
       }
     }
-    nmc_dma16(zl_src(i0, 0), zl + (2 * ((i0 * P) & 1)) * 64);
+    put_zl(gs0);
+    put_zl(gs0 + 1);
     for (int s = 0; s < 2; ++s)   // x + (-0.0) == x: the fixed slot sum
       for (int j = 0; j < Fam::NACC; ++j)
         for (int k = TI.nt; k < NMC_NSLOT; ++k)
@@ -224,6 +245,41 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
   }
   __syncthreads();
   NMC_SL(1);
+
+  // the proposal of step k (Parameter.propose :304-306) and its likelihood registers:
+  // th with th[p] = prop (this lane's chain, and the partner lane's for the paired rows)
+  auto proposal = [&](const double (&thv)[MP], int p, double prop, Reg& reg, Reg& preg) {
+    double thp[MP];
+#pragma unroll
+    for (int q = 0; q < MP; ++q) thp[q] = q == p ? prop : thv[q];
+    reg = fam.prepare(thp);
+    preg = reg;
+    if constexpr (PAIRED_OK) if (paired) {
+      const bool hi = lane >= 32;
+#pragma unroll
+      for (int q = 0; q < MP; ++q) {
+        const nmc_pair2 e = nmc_halves(thp[q]);
+        thp[q] = hi ? e.lo : e.hi;
+      }
+      preg = fam.prepare(thp);
+    }
+  };
+  auto sel = [](const double (&a)[MP], int p) {
+    double v = a[0];
+#pragma unroll
+    for (int q = 1; q < MP; ++q)
+      if (q == p) v = a[q];
+    return v;
+  };
+  // step gs0's proposal
+  double prop, lu;
+  Reg reg, preg;
+  {
+    const double* z0 = zl + (2 * (gs0 & 3)) * 64 + 2 * lane;
+    prop = th[0] + (1.0 * sc[0]) * z0[0];
+    lu = z0[1];
+    proposal(th, 0, prop, reg, preg);
+  }
 
   bool ok = true;
   int pub_p = -1;                    // control wave: published value awaiting its count
@@ -261,21 +317,12 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
       pub_p = -1;
     }
   };
-  auto sel = [](const double (&a)[MP], int p) {
-    double v = a[0];
-#pragma unroll
-    for (int q = 1; q < MP; ++q)
-      if (q == p) v = a[q];
-    return v;
-  };
 
-  const int gs0 = i0 * P;
   for (int t = i0; t < i1 && ok; ++t) {
     const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
     for (int p = 0; p < P; ++p) {
       const int gs = t * P + p, sp = gs & 1;
       double* opk = ops + sp * 4 * 64;
-      const double* zk = zl + (2 * sp) * 64 + 2 * lane;
       const bool due = PARTIAL && gs - lag >= gs0;   // the Gibbs wave's task gs - lag
       const bool post_prior = due && P <= 2;         // ... is the update this step's prior needs
       const double thp_p = sel(th, p), scp = sel(sc, p);
@@ -284,7 +331,7 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
 
       // ---- Gibbs wave: task gs - lag = (kt, kq), and this step's priors when due ----
       if constexpr (PARTIAL) if (gw && due) {
-        if (W > 1 && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
+        if (!(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
         const int k = gs - lag, kq = k % P, kt = k / P;
         const bool r = nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1));
         if (lane == 0)
@@ -293,9 +340,10 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
         if (r) {
           // keep the payload loads below the poll (no instruction: wavefront scope)
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          nmc_hyper_update_reg(d, cb, kt, kq, cc, lds, L.hyp, g0w);
+          double xv[64], hz, hx;
+          nmc_hyper_fetch_reg(d, kt, kq, cc, xv, hz, hx);
+          nmc_hyper_compute_reg(d, cb, kt, kq, lds, L.hyp, g0w, hz, hx, xv);
           if (post_prior) {
-            const double prop = thp_p + (1.0 * scp) * zk[0];
             const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
             const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
             opk[NMC_OP_LPC * 64] =
@@ -303,11 +351,11 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
             opk[NMC_OP_LPP * 64] = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
           }
         }
-        if (W > 1) __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
       }
-      // ---- control wave: bookkeeping of step gs-1, operands of this step, next z ----
+      // ---- control wave: bookkeeping of step gs-1, operands of this step, z of gs+2 ----
       if (ctl) {
-        if (W > 1 && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
+        if (!(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
         if (pend_p >= 0) apply_pending();
         {
           const double na = st[(NMC_ST_NA * P + p) * 64], nr = st[(NMC_ST_NR * P + p) * 64];
@@ -326,7 +374,6 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
           opk[NMC_OP_SR * 64] = sR;
         }
         if (!post_prior) {   // priors (:293-294)
-          const double prop = thp_p + (1.0 * scp) * zk[0];
           double lpc, lpp;
           if constexpr (PARTIAL) {
             const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
@@ -342,34 +389,31 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
         }
         // the previous step's published value has had the work above to drain
         if constexpr (PARTIAL) count_published();
-        const int tn = p + 1 < P ? t : t + 1;
-        const int pn = p + 1 < P ? p + 1 : 0;
-        if (tn < i1) nmc_dma16(zl_src(tn, pn), zl + (2 * (sp ^ 1)) * 64);
-        if (W > 1) __builtin_amdgcn_s_setprio(0);
+        put_zl(gs + 2);
+        __builtin_amdgcn_s_setprio(0);
       }
 
-      // ---- every wave: the proposal and its likelihood tiles ----
+      // ---- every wave: the likelihood tiles of the proposal (:615-635) ----
       NMC_SW(si, 1);
-      const double lu = zk[1];
-      const double prop = thp_p + (1.0 * scp) * zk[0];   // Parameter.propose (:304-306)
-      double thp[MP];
-#pragma unroll
-      for (int q = 0; q < MP; ++q) thp[q] = q == p ? prop : th[q];
-      const typename Fam::Reg reg = fam.prepare(thp);
-      typename Fam::Reg preg = reg;   // paired rows: the partner lane's (lane ^ 32) proposal
-      if constexpr (nmc_paired_rows_ok<Fam>()) if (d.paired) {
-        const bool hi = lane >= 32;
-        double pth[MP];
-#pragma unroll
-        for (int q = 0; q < MP; ++q) {
-          const nmc_pair2 e = nmc_halves(thp[q]);
-          pth[q] = hi ? e.lo : e.hi;
-        }
-        preg = fam.prepare(pth);
-      }
       nmc_step_tiles(d, fam, reg, preg, lrows, TI, tcnt + sp,
                      lds + (L.part + sp * Fam::NACC * NMC_NSLOT) * 64 + lane, si);
-      if (ctl) nmc_drain_vm();   // the next step's {z, log u} have landed
+      // ---- the next step's proposal for both outcomes of this decision (P >= 2: the
+      //      next parameter's value and scale are already known; its z landed before the
+      //      previous barrier) ----
+      const int pn = p + 1 < P ? p + 1 : 0;
+      double propn = 0.0, lun = 0.0;
+      Reg regA = reg, regR = reg, pregA = preg, pregR = preg;
+      if (P >= 2 && gs + 1 < ge) {
+        const double* zn = zl + (2 * ((gs + 1) & 3)) * 64 + 2 * lane;
+        propn = sel(th, pn) + (1.0 * sel(sc, pn)) * zn[0];
+        lun = zn[1];
+        double thA[MP];
+#pragma unroll
+        for (int q = 0; q < MP; ++q) thA[q] = q == p ? prop : th[q];
+        proposal(thA, pn, propn, regA, pregA);
+        proposal(th, pn, propn, regR, pregR);
+      }
+      if (ctl) nmc_drain_vm();   // step gs+2's {z, log u} have landed
       NMC_SW(si, 2);
       __syncthreads();
       NMC_SW(si, 3);
@@ -414,6 +458,19 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
         pend_p = p;
         pend_t = t;
       }
+      // the next step's proposal: selected (P >= 2) or formed now (P == 1: it depends on
+      // this decision's value and scale)
+      if (P >= 2) {
+        prop = propn;
+        lu = lun;
+        reg = nmc_reg_select(accept, regA, regR);
+        if constexpr (PAIRED_OK) if (paired) preg = nmc_reg_select(accept, pregA, pregR);
+      } else if (gs + 1 < ge) {
+        const double* zn = zl + (2 * ((gs + 1) & 3)) * 64 + 2 * lane;
+        prop = th[0] + (1.0 * sc[0]) * zn[0];
+        lu = zn[1];
+        proposal(th, 0, prop, reg, preg);
+      }
       NMC_SW(si, 4);
       if (due) {
         ok = verdict == 2.0 * ((double)gs + 1);
@@ -446,11 +503,13 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
   // ---- closing Gibbs updates, tasks ge-lag .. ge-1 (group-0 workgroups write and record
   //      them), once every workgroup of the chain block has published its last value ----
   if constexpr (PARTIAL) if (ok && g0w) {
-    const int ge = i1 * P;
     if (nmc_wait_published_col(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L.flag) &&
         gw) {
-      for (int k = ge - lag > gs0 ? ge - lag : gs0; k < ge; ++k)
-        nmc_hyper_update_reg(d, cb, k / P, k % P, cc, lds, L.hyp, true);
+      for (int k = ge - lag > gs0 ? ge - lag : gs0; k < ge; ++k) {
+        double xv[64], hz, hx;
+        nmc_hyper_fetch_reg(d, k / P, k % P, cc, xv, hz, hx);
+        nmc_hyper_compute_reg(d, cb, k / P, k % P, lds, L.hyp, true, hz, hx, xv);
+      }
     }
   }
   nmc_drain_vm();
