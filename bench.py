@@ -30,7 +30,10 @@ import numpy  # noqa: E402
 METRIC = ("MCMC iterations/sec (all chains×groups) + achieved HBM GB/s, "
           "1/2/4/8 MI355X")
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X fp64 vector (half the f32 vector rate, 157.3 TF)
+# fp64 VALU issue: 256 CUs x 4 SIMDs x 16 fp64 lanes x 2.4 GHz lane-instructions per second
+# (the 78.6 TFLOP/s fp64 vector peak counts an FMA as 2 flops)
+VALU_PEAK_TIPS = 256 * 4 * 16 * 2.4e9 / 1e12
+VALU_PER_CHAIN_ROW = 3          # fp64 VALU lane-instructions per (chain, row, parameter step)
 
 
 def parse():
@@ -96,13 +99,13 @@ def cpu_baseline(args, budget_s):
            "sample": "%d chains x %d iterations of the cfg-3 workload (%d groups x %d obs, "
                      "partial pooling) in the numpy oracle, one process per chain"
                      % (cores, iters, args.groups, args.obs)}
-    cal = os.path.join(ROOT, "profiles", "cpu_calibration_r02.json")
+    cal = os.path.join(ROOT, "profiles", "cpu_calibration_r03.json")
     if os.path.exists(cal):
         # the reference cannot travel to this box: its speed relative to the restatement
         # was measured side by side in the build container (oracle/calibrate_cpu.py)
         ratio = json.load(open(cal))["reference_over_restatement"]
         out["calibration"] = {"reference_over_restatement": ratio,
-                              "source": "profiles/cpu_calibration_r02.json "
+                              "source": "profiles/cpu_calibration_r03.json "
                                         "(oracle/calibrate_cpu.py, build container)"}
         out["reference_equivalent_value"] = rate * ratio
     return out
@@ -279,21 +282,30 @@ def main():
     avg_step_ms = kt["step_ms"] / max(1, launches)
     iters_per_launch = kt["step_iters"] / max(1, launches)
     b_obs = fam.bytes_per_obs()
+    lc = eng.launch_config()
     # B_unit = P*N*b_obs per chain*group*iteration (each parameter step
     # evaluates the group's rows once per chain).  The rows are LDS-resident for the
-    # launch: every chain-lane receives each row from an LDS broadcast read, so these
-    # are the bytes the LDS delivers -- the binding resource -- not HBM bytes.
+    # launch, so these bytes never come from HBM; they are the rows delivered to the
+    # chain lanes.
     bytes_per_launch = C * G * P * N * b_obs * iters_per_launch
     achieved_gbs = bytes_per_launch / (avg_step_ms * 1e-3) / 1e9
-    # fp64 work: fma + sub + fma = 5 flops per (chain, obs, parameter step)
-    flops_per_launch = C * G * P * N * 5 * iters_per_launch
-    fp64_tflops = flops_per_launch / (avg_step_ms * 1e-3) / 1e12
+    # The binding resource is fp64 VALU issue.  The shipped row loop (kernels.h
+    # nmc_rows_lds_linreg2_paired; profiles/isa_r03_linreg_paired.txt) issues 24 fp64 VALU
+    # instructions (v_add_f64 x8, v_fma_f64 x16) per 8-row block for two chains per lane:
+    # 3 per (chain, row, parameter step) -- the whole likelihood work.  achieved = those
+    # lane-instructions per second; peak = 256 CUs x 4 SIMDs x 16 fp64 lanes x 2.4 GHz
+    # (= the 78.6 TFLOP/s fp64 vector peak / 2 flops per FMA).
+    lane_instr_per_launch = C * G * P * N * VALU_PER_CHAIN_ROW * iters_per_launch
+    valu_tips = lane_instr_per_launch / (avg_step_ms * 1e-3) / 1e12
+    # LDS bytes actually delivered: one ds_read_b128 serves a row pair to the 64 lanes, i.e.
+    # each (row, chain pair) once -- half the algorithmic bytes in the paired loop
+    lds_delivered = bytes_per_launch / (2.0 if lc.get("kernel", "").find("Linreg<2>") >= 0 else 1.0)
+    lds_gbs = lds_delivered / (avg_step_ms * 1e-3) / 1e9
     traffic, hbm_meas = None, None
     if pmc and "bytes_per_launch" in pmc:
         # measured for a K-iteration launch; scaled if this run's launches differ
         traffic = pmc["bytes_per_launch"] * iters_per_launch / pmc["iterations_per_launch"]
         hbm_meas = traffic / (avg_step_ms * 1e-3) / 1e9
-    lc = eng.launch_config()
     kname = lc["kernel"]
 
     if rank == 0:
@@ -315,17 +327,23 @@ def main():
                        "chains_per_gpu": C, "groups": G, "obs_per_group": N, "params": P,
                        "pooling": "partial", "parallelism": "chains sharded x%d" % world,
                        "launch": lc},
-            "roofline": {"bound": "lds", "achieved": achieved_gbs, "peak": LDS_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved_gbs / LDS_PEAK_GBS,
+            "roofline": {"bound": "valu", "achieved": valu_tips, "peak": VALU_PEAK_TIPS,
+                         "unit": "T fp64 lane-instr/s", "frac": valu_tips / VALU_PEAK_TIPS,
                          "traffic": traffic,
                          "kernel": kname,
                          "avg_launch_us": avg_step_ms * 1e3,
                          "iterations_per_launch": iters_per_launch,
-                         "algorithmic_bytes_per_launch": bytes_per_launch,
-                         "derivation": "achieved = C*G*P*N*b_obs*iterations_per_launch / "
-                                       "avg_launch_us (SURVEY 8(d) bytes, delivered by LDS "
-                                       "broadcast reads); peak = 256 B/clk/CU x 256 CUs x "
-                                       "2.4 GHz (MI355X_MICROARCH.md LDS)",
+                         "valu_lane_instr_per_launch": lane_instr_per_launch,
+                         "derivation": "achieved = C*G*P*N*3 fp64 VALU lane-instructions per "
+                                       "iteration (the shipped paired row loop: 24 per 8-row "
+                                       "block per 2 chains) x iterations_per_launch / "
+                                       "avg_launch_us; peak = 256 CUs x 4 SIMDs x 16 fp64 lanes "
+                                       "x 2.4 GHz (78.6 TFLOP/s fp64 / 2)",
+                         "lds": {"delivered_gbs": lds_gbs, "peak": LDS_PEAK_GBS,
+                                 "frac": lds_gbs / LDS_PEAK_GBS,
+                                 "note": "bytes the ds_read_b128 of the paired loop deliver "
+                                         "(each serves a row pair to 64 lanes = 2 chains per "
+                                         "row): half of C*G*P*N*b_obs"},
                          "hbm": {"algorithmic_gbs": achieved_gbs, "peak": HBM_PEAK_GBS,
                                  "algorithmic_frac": achieved_gbs / HBM_PEAK_GBS,
                                  "measured_gbs": hbm_meas,
@@ -335,9 +353,6 @@ def main():
                                          "read from HBM once per launch and served from LDS, "
                                          "so the algorithmic frac exceeds 1 by construction; "
                                          "measured = PMC bytes of the same launch"},
-                         "fp64_valu": {"achieved": fp64_tflops, "peak": FP64_VALU_PEAK_TFLOPS,
-                                       "unit": "TFLOP/s",
-                                       "frac": fp64_tflops / FP64_VALU_PEAK_TFLOPS},
                          "pmc": pmc},
             "cpu_baseline": cpu,
             "event_ms": ev_ms,

@@ -90,7 +90,7 @@ static inline bool uses_step(const nmc_ctx* x, int mode) {
 }
 static inline size_t step_lds_bytes(const nmc_ctx* x) {
   return (size_t)nmc_step_lds(x->nacc, x->d.P, x->pooling == NMC_POOL_PARTIAL,
-                              x->d.nmax * x->nf).total * 512;
+                              x->d.nmax * x->nf, x->d.G).total * 512;
 }
 
 static inline size_t run_lds_bytes(const nmc_ctx* x) {

@@ -75,7 +75,8 @@ static int nmc_fam_call(nmc_ctx* x, const Fam& fam, NmcCall& c) {
       const double* in = c.in;
       double* aux = c.aux;
       void* a1[] = {&dd, (void*)&fam, (void*)&obs, (void*)&in, (void*)&aux};
-      HIPCHK(hipLaunchKernel(k, dim3(d.CB * d.G * d.S), dim3(64 * d.W), a1, lds, x->stream));
+      HIPCHK(hipLaunchKernel(k, dim3(d.CB * d.G * d.S), dim3(64 * std::min(d.W, 8)), a1, lds,
+                             x->stream));
       const size_t n = (size_t)d.G * d.C;
       hipLaunchKernelGGL(nmc_k_group_fin<Fam>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                          x->stream, d, fam, c.in, (const double*)c.aux, c.out);

@@ -94,6 +94,8 @@ struct Dev {
   int hlds, naux;        // persistent partial: Gibbs payload via LDS, auxiliary waves
   int hreg;              // persistent partial, G <= 64: Gibbs payload in registers (SYNC_REG)
   int noprio;            // diagnostics: no issue priority for the latency-bound waves
+  int sflags;            // nmc_k_step variants (bit-identical; NMC_STEP_FLAGS): 1 Gibbs payload
+                         // via LDS-DMA, 2 next proposal formed before the barrier
   int rows_lds;          // 1: each workgroup stages its group's rows in LDS once per launch
   int tile;              // target rows per likelihood tile (nmc_tiles)
   unsigned* cnt;         // [CB][P][32] publish counters (persistent partial), zeroed per launch
@@ -569,7 +571,8 @@ __device__ __forceinline__ void nmc_ll_rows(const Fam& fam, const typename Fam::
 
 // The regression row loop (FamLinreg<2>: rows {x, y}, e = fma(x, b1, b0 - y),
 // acc[i & 3] = fma(e, e, acc[i & 3]) for row i of each 8-row block) written by hand:
-// two fixed register sets v[192:223] / v[224:255], block b+1's eight broadcast
+// two fixed register sets v[104:135] / v[136:167] (below 168, so the step kernel can run
+// three waves per SIMD), block b+1's eight broadcast
 // ds_read_b128 in flight while block b is consumed (counted lgkmcnt(8)).  The compiler
 // does not keep this prefetch (it sinks the reads below the arithmetic and copies the
 // register sets); measured at the LDS-broadcast floor, ~5 cycles per row per CU
@@ -603,31 +606,31 @@ __device__ __forceinline__ void nmc_rows_lds_linreg2(const double* p, int nb, do
   unsigned addr = (unsigned)(uintptr_t)(nmc_lds_cptr)p;
   int cnt = nb;
   asm volatile(
-      NMC_L8(192, 0)
+      NMC_L8(104, 0)
       "L_nmc_rows_%=:\n"
-      NMC_L8(224, 128)
+      NMC_L8(136, 128)
       "s_waitcnt lgkmcnt(8)\n"
-      NMC_B8(192)
+      NMC_B8(104)
       "v_add_u32 %[addr], 0x100, %[addr]\n"
       "s_sub_u32 %[cnt], %[cnt], 2\n"
       "s_cmp_gt_i32 %[cnt], 0\n"
       "s_cbranch_scc0 L_nmc_last_%=\n"
-      NMC_L8(192, 0)
+      NMC_L8(104, 0)
       "s_waitcnt lgkmcnt(8)\n"
-      NMC_B8(224)
+      NMC_B8(136)
       "s_branch L_nmc_rows_%=\n"
       "L_nmc_last_%=:\n"
       "s_waitcnt lgkmcnt(0)\n"
-      NMC_B8(224)
+      NMC_B8(136)
       : [addr] "+v"(addr), [cnt] "+s"(cnt), [a0] "+v"(a0), [a1] "+v"(a1), [a2] "+v"(a2),
         [a3] "+v"(a3)
       : [b0] "v"(b0), [b1] "v"(b1)
-      : "v192", "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200", "v201", "v202",
-        "v203", "v204", "v205", "v206", "v207", "v208", "v209", "v210", "v211", "v212", "v213",
-        "v214", "v215", "v216", "v217", "v218", "v219", "v220", "v221", "v222", "v223", "v224",
-        "v225", "v226", "v227", "v228", "v229", "v230", "v231", "v232", "v233", "v234", "v235",
-        "v236", "v237", "v238", "v239", "v240", "v241", "v242", "v243", "v244", "v245", "v246",
-        "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255", "scc", "memory");
+      : "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114",
+        "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125",
+        "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136",
+        "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147",
+        "v148", "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158",
+        "v159", "v160", "v161", "v162", "v163", "v164", "v165", "v166", "v167", "scc", "memory");
 }
 
 // The paired-chain form of the same loop (NMC_ROWS_PAIRED): lanes 0-31 read row 2m and
@@ -674,30 +677,30 @@ __device__ __forceinline__ void nmc_rows_lds_linreg2_paired(const double* p, int
   unsigned addr = (unsigned)(uintptr_t)(nmc_lds_cptr)p;
   int cnt = nb;
   asm volatile(
-      NMC_P4(208, 0)
+      NMC_P4(120, 0)
       "L_nmc_prows_%=:\n"
-      NMC_P4(232, 128)
+      NMC_P4(144, 128)
       "s_waitcnt lgkmcnt(4)\n"
-      NMC_PB(208, 224)
+      NMC_PB(120, 136)
       "v_add_u32 %[addr], 0x100, %[addr]\n"
       "s_sub_u32 %[cnt], %[cnt], 2\n"
       "s_cmp_gt_i32 %[cnt], 0\n"
       "s_cbranch_scc0 L_nmc_plast_%=\n"
-      NMC_P4(208, 0)
+      NMC_P4(120, 0)
       "s_waitcnt lgkmcnt(4)\n"
-      NMC_PB(232, 248)
+      NMC_PB(144, 160)
       "s_branch L_nmc_prows_%=\n"
       "L_nmc_plast_%=:\n"
       "s_waitcnt lgkmcnt(0)\n"
-      NMC_PB(232, 248)
+      NMC_PB(144, 160)
       : [addr] "+v"(addr), [cnt] "+s"(cnt), [u0] "+v"(u0), [u1] "+v"(u1), [w0] "+v"(w0),
         [w1] "+v"(w1)
       : [b0] "v"(b0), [b1] "v"(b1), [c0] "v"(c0), [c1] "v"(c1)
-      : "v208", "v209", "v210", "v211", "v212", "v213", "v214", "v215", "v216", "v217", "v218",
-        "v219", "v220", "v221", "v222", "v223", "v224", "v225", "v226", "v227", "v228", "v229",
-        "v230", "v231", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240",
-        "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251",
-        "v252", "v253", "v254", "v255", "scc", "memory");
+      : "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130",
+        "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141",
+        "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152",
+        "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161", "v162", "v163",
+        "v164", "v165", "v166", "v167", "scc", "memory");
 }
 
 // The same over rows staged in LDS: blocks of R rows read with wave-uniform

@@ -119,6 +119,7 @@ static void choose_geometry(nmc_ctx* x) {
   // the one-barrier step kernel (step.h) where it applies; NMC_STEP=0 keeps nmc_k_run
   // (bit-identical: the tests compare the two)
   x->step_ok = !(getenv("NMC_STEP") && atoi(getenv("NMC_STEP")) == 0);
+  d.sflags = getenv("NMC_STEP_FLAGS") ? atoi(getenv("NMC_STEP_FLAGS")) : 0;
 }
 
 // numpy's pairwise-sum recursion over G groups (numpy/_core/src/umath/loops_utils.h):
@@ -345,6 +346,19 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     // row split: always persistent (the members exchange every step), in resident batches
     // of chain blocks when the whole grid is not (chain blocks are independent)
     x->persistent = c.result == 1 || d.S > 1;
+  }
+  // the one-barrier step kernel runs up to 12 waves (three per SIMD) when its grid is one
+  // workgroup per CU: two likelihood waves per SIMD keep the fp64 pipe busy while the
+  // third plays a role (NMC_STEP_WAVES overrides; the tile partition, and every sum, does
+  // not depend on the wave count)
+  if (uses_step(x, run_mode(x)) && (int64_t)d.RB * d.G * d.S <= x->ncu) {
+    int w = 1 + (int)((d.nmax + 63) / 64) + (pooling == NMC_POOL_PARTIAL ? 1 : 0);
+    w = std::min(w, NMC_STEP_THREADS / 64);
+    if (const char* e = getenv("NMC_STEP_WAVES")) {
+      const int v = atoi(e);
+      if (v >= 3 && v <= NMC_STEP_THREADS / 64) w = v;
+    }
+    if (w > d.W) d.W = w;
   }
   if (d.S > 1) {   // row split: resident batches of chain blocks, exchange buffers
     NmcCall c;

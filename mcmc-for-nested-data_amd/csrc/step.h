@@ -42,12 +42,13 @@ struct nmc_step_layout {
   int hyp;    // [6][P]            hyper state (NMC_HY_*), partial pooling
   int zl;     // [4][2]            {z, log u} ring by step (LDS-DMA, two steps ahead)
   int ops;    // [2][4]            decision operands by step parity (NMC_OP_*)
+  int hval;   // [G + 1]           Gibbs payload: the chain block's values of one parameter
   int flag;   // [1]               wait flag, Gibbs verdict, tile counters
   int rows;   // [nmax][NF]        the group's rows, staged once per launch
   int total;
 };
 __host__ __device__ inline nmc_step_layout nmc_step_lds(int nacc, int P, int partial,
-                                                        int row_doubles) {
+                                                        int row_doubles, int G) {
   nmc_step_layout L;
   L.part = 0;
   L.st = L.part + 2 * nacc * NMC_NSLOT;
@@ -55,7 +56,8 @@ __host__ __device__ inline nmc_step_layout nmc_step_lds(int nacc, int P, int par
   L.hyp = L.cw + 5;
   L.zl = L.hyp + (partial ? 6 * P : 0);
   L.ops = L.zl + 8;
-  L.flag = L.ops + 8;
+  L.hval = L.ops + 8;
+  L.flag = L.hval + (partial ? G + 1 : 0);   // (+1: the payload DMA moves group pairs)
   L.rows = L.flag + 1;
   // (+1 column: the pipelined row loops prefetch one block past a tile's rows)
   L.total = L.rows + (row_doubles > 0 ? (row_doubles + 63) / 64 + 1 : 0);
@@ -156,8 +158,15 @@ __device__ __forceinline__ R nmc_reg_select(bool a, const R& x, const R& y) {
   return r;
 }
 
+// (768 threads: up to three waves per SIMD -- the hand-written row loops keep below v168 --
+//  so two likelihood waves per SIMD issue fp64 while the third plays a role; one wave alone
+//  issues an fp64 instruction at most every ~7 cycles, two every ~3.4: tools/fp64lat.hip,
+//  tools/llbench7.hip)
+#ifndef NMC_STEP_THREADS
+#define NMC_STEP_THREADS 512
+#endif
 template <class Fam, int MODE>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(NMC_STEP_THREADS)
 nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int flags) {
   static_assert(MODE == NMC_MODE_NOPOOL || MODE == NMC_MODE_SYNC_REG,
                 "nmc_k_step: none/complete pooling or the register Gibbs hand-off");
@@ -177,11 +186,14 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
   const int cc = c < C ? c : C - 1;
   const int ngrp = (int)(d.off[g + 1] - d.off[g]);
   const nmc_tiling TI = nmc_tiles(ngrp, d.tile);
-  const nmc_step_layout L = nmc_step_lds(Fam::NACC, P, PARTIAL, d.nmax * Fam::NFIELDS);
+  const nmc_step_layout L = nmc_step_lds(Fam::NACC, P, PARTIAL, d.nmax * Fam::NFIELDS, G);
   const size_t PGC = (size_t)P * G * C;
   const size_t gc = (size_t)g * C + cc;
   const bool ctl = w == 0;
   const bool gw = PARTIAL && w == 1;       // the Gibbs wave (host: W >= 3, G <= 64)
+  nmc_lds_layout HL;                       // (the Gibbs helpers' view: payload, hyper state)
+  HL.hval = L.hval;
+  HL.hyp = L.hyp;
   const int lag = P >= 2 ? 2 : 1;          // Gibbs task of step gs: gs - lag
   const bool paired = PAIRED_OK && d.paired;
   double* st = lds + L.st * 64 + lane;     // st[(k * P + p) * 64]
@@ -308,6 +320,22 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
     }
     pend_p = -1;
   };
+  // the Gibbs update of parameter kq after iteration kt (HyperParameter.update :463-498) for
+  // this wave's 64 chains: the chain block's published values -> LDS payload (sc1 LDS-DMA,
+  // one round trip), numpy's pairwise sums read back from LDS (nmc_hyper_compute)
+  auto gibbs_task = [&](int kt, int kq, bool write) {
+    const size_t hvi = (((size_t)(kt - d.vbase) * P + kq) * C + cc) * 2;
+    const double hz = d.vh[hvi], hx = d.vh[hvi + 1];
+    const double* src = (kt & 1) ? d.vb1 : d.vb0;
+    if ((C & 1) == 0) {
+      nmc_hyper_dma(d, src, kq, cb, 0, G, lds, HL, 0);
+      nmc_drain_vm();
+    } else {
+      nmc_hyper_load(d, src, kq, cc, 0, G, lds, HL, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    nmc_hyper_compute(d, cb, kt, kq, lds, HL, write, hz, hx, 0);
+  };
   auto count_published = [&]() {
     if (pub_p >= 0) {
       nmc_drain_vm();
@@ -340,9 +368,13 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
         if (r) {
           // keep the payload loads below the poll (no instruction: wavefront scope)
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          double xv[64], hz, hx;
-          nmc_hyper_fetch_reg(d, kt, kq, cc, xv, hz, hx);
-          nmc_hyper_compute_reg(d, cb, kt, kq, lds, L.hyp, g0w, hz, hx, xv);
+          if (d.sflags & 1) {
+            gibbs_task(kt, kq, g0w);
+          } else {
+            double xv[64], hz, hx;
+            nmc_hyper_fetch_reg(d, kt, kq, cc, xv, hz, hx);
+            nmc_hyper_compute_reg(d, cb, kt, kq, lds, L.hyp, g0w, hz, hx, xv);
+          }
           if (post_prior) {
             const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
             const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
@@ -403,7 +435,8 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
       const int pn = p + 1 < P ? p + 1 : 0;
       double propn = 0.0, lun = 0.0;
       Reg regA = reg, regR = reg, pregA = preg, pregR = preg;
-      if (P >= 2 && gs + 1 < ge) {
+      const bool pre = (d.sflags & 2) && P >= 2;
+      if (pre && gs + 1 < ge) {
         const double* zn = zl + (2 * ((gs + 1) & 3)) * 64 + 2 * lane;
         propn = sel(th, pn) + (1.0 * sel(sc, pn)) * zn[0];
         lun = zn[1];
@@ -460,16 +493,20 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
       }
       // the next step's proposal: selected (P >= 2) or formed now (P == 1: it depends on
       // this decision's value and scale)
-      if (P >= 2) {
+      if (pre) {
         prop = propn;
         lu = lun;
         reg = nmc_reg_select(accept, regA, regR);
-        if constexpr (PAIRED_OK) if (paired) preg = nmc_reg_select(accept, pregA, pregR);
+        if constexpr (PAIRED_OK) if (paired) {   // the partner lane's (lane ^ 32) outcome
+          const unsigned a = accept ? 1u : 0u;
+          const auto sw = __builtin_amdgcn_permlane32_swap(a, a, false, false);
+          preg = nmc_reg_select((lane >= 32 ? sw[0] : sw[1]) != 0u, pregA, pregR);
+        }
       } else if (gs + 1 < ge) {
         const double* zn = zl + (2 * ((gs + 1) & 3)) * 64 + 2 * lane;
-        prop = th[0] + (1.0 * sc[0]) * zn[0];
+        prop = sel(th, pn) + (1.0 * sel(sc, pn)) * zn[0];
         lu = zn[1];
-        proposal(th, 0, prop, reg, preg);
+        proposal(th, pn, prop, reg, preg);
       }
       NMC_SW(si, 4);
       if (due) {
@@ -506,9 +543,13 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
     if (nmc_wait_published_col(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L.flag) &&
         gw) {
       for (int k = ge - lag > gs0 ? ge - lag : gs0; k < ge; ++k) {
-        double xv[64], hz, hx;
-        nmc_hyper_fetch_reg(d, k / P, k % P, cc, xv, hz, hx);
-        nmc_hyper_compute_reg(d, cb, k / P, k % P, lds, L.hyp, true, hz, hx, xv);
+        if (d.sflags & 1) {
+          gibbs_task(k / P, k % P, true);
+        } else {
+          double xv[64], hz, hx;
+          nmc_hyper_fetch_reg(d, k / P, k % P, cc, xv, hz, hx);
+          nmc_hyper_compute_reg(d, cb, k / P, k % P, lds, L.hyp, true, hz, hx, xv);
+        }
       }
     }
   }

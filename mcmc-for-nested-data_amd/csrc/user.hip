@@ -237,7 +237,8 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
       double* out = c.out;
       void* a1[] = {&dd, &fam, (void*)&obs, (void*)&in, (void*)&aux};
       if (int rc = user_fn(x, d0.rows_lds ? UK_GROUP_LL_RL : UK_GROUP_LL, &f)) return rc;
-      if (int rc = launch(x, f, dim3(d0.CB * d0.G * d0.S), dim3(64 * d0.W), nmc_group_ll_lds(x), a1))
+      if (int rc = launch(x, f, dim3(d0.CB * d0.G * d0.S), dim3(64 * std::min(d0.W, 8)),
+                          nmc_group_ll_lds(x), a1))
         return rc;
       const size_t n = (size_t)d0.G * d0.C;
       void* a2[] = {&dd, &fam, (void*)&in, (void*)&aux, (void*)&out};

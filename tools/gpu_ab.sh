@@ -1,22 +1,19 @@
 #!/bin/bash
-# A/B of step-kernel geometries on one MI355X: the GPU tests (optional -k filter), then
-# the bench line without the CPU leg and PMC passes once per environment setting.
-#   usage: tools/gpu_ab.sh TAG "pytest -k expr or empty" "ENV=V ENV2=V" "ENV=V" ...
+# A/B of step-kernel builds on one box: each variant runs the driver's bench command and the
+# default-length bench (no PMC, no CPU leg).  usage: tools/gpu_ab.sh TAG "NAME:ENV ..."
 set -o pipefail
-TAG=${1:-ab}; K=${2:-}; shift 2
-cd "$GRAFT_REPO_ROOT" || exit 1
+TAG=$1; shift
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-if [ "$K" != "none" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
-      -p no:cacheprovider ${K:+-k "$K"} > gpurun_out/tests_$TAG.log 2>&1
-  rc=$?
-  tail -3 gpurun_out/tests_$TAG.log
-  [ $rc -eq 0 ] || exit $rc
-fi
-i=0
-for e in "$@"; do
-  i=$((i+1))
-  env $e timeout -k 10 200 python bench.py --cpu-seconds 0 --no-pmc > gpurun_out/bench_${TAG}_$i.json 2> gpurun_out/bench_${TAG}_$i.err || exit $?
-  python3 -c "import json,sys;d=json.load(open('gpurun_out/bench_${TAG}_$i.json'));print(sys.argv[1], 'value %.4g  us/iter %.3f  kernel us/launch %.0f' % (d['value'], d['ms_per_step']*1e3, d['roofline']['avg_launch_us']), d['config']['launch'])" "$e"
+for v in "$@"; do
+  name=${v%%:*}; envs=${v#*:}
+  echo "== $name ($envs) $(date +%T)"
+  env $envs timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-pmc --cpu-seconds 0 \
+      > gpurun_out/ab_${TAG}_${name}_20.json 2> gpurun_out/ab_${TAG}_${name}_20.err || exit $?
+  env $envs timeout -k 10 200 python3 bench.py --no-pmc --cpu-seconds 0 \
+      > gpurun_out/ab_${TAG}_${name}.json 2> gpurun_out/ab_${TAG}_${name}.err || exit $?
+  python3 -c "
+import json,sys
+a=json.load(open('gpurun_out/ab_${TAG}_${name}_20.json')); b=json.load(open('gpurun_out/ab_${TAG}_${name}.json'))
+print('$name', 'bench20 %.4g' % a['value'], 'bench2000 %.4g' % b['value'], 'kernel_us/iter %.3f' % (b['roofline']['avg_launch_us']/b['roofline']['iterations_per_launch']), b['config']['launch']['waves_per_group'], b['roofline']['kernel'])"
 done
