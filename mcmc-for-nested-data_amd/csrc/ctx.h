@@ -59,7 +59,7 @@ struct nmc_ctx {
   bool tmo_clean = false;                 // timeout flag read clear, no launch since
   void* user = nullptr;                   // user family: its per-device kernel table (user.hip)
   double* user_k = nullptr;               // user family: device copy of the model constants
-  bool step_ok = true;                    // nmc_k_step where it applies (NMC_STEP=0: nmc_k_run)
+  bool step_ok = false;                   // nmc_k_step where it applies (NMC_STEP=1)
 };
 
 static inline double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->d.vb0; }

@@ -116,9 +116,10 @@ static void choose_geometry(nmc_ctx* x) {
   // reads; NMC_ROWS=bcast keeps the one-chain broadcast loop (same sums bit for bit)
   d.paired = d.rows_lds && x->nf <= 4;
   if (const char* e = getenv("NMC_ROWS")) d.paired = d.paired && strcmp(e, "bcast") != 0;
-  // the one-barrier step kernel (step.h) where it applies; NMC_STEP=0 keeps nmc_k_run
-  // (bit-identical: the tests compare the two)
-  x->step_ok = !(getenv("NMC_STEP") && atoi(getenv("NMC_STEP")) == 0);
+  // nmc_k_step (one barrier per step, every wave deciding) measured slower than nmc_k_run
+  // on MI355X (cfg 3: 8.8 against 8.0 us/iter, profiles/r03_step_kernel_ab.json): opt-in,
+  // NMC_STEP=1, bit-identical (tests/test_gpu_scale.py)
+  x->step_ok = getenv("NMC_STEP") && atoi(getenv("NMC_STEP")) != 0;
   d.sflags = getenv("NMC_STEP_FLAGS") ? atoi(getenv("NMC_STEP_FLAGS")) : 0;
 }
 

@@ -193,15 +193,20 @@ def test_eval_group_ll_matches_oracle(gpu_lib):
 def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
     """The paired-chain row loop (each lane evaluates its row pair half for its own chain
     and for lane ^ 32's, kernels.h nmc_ll_rows_lds<Fam, true>) reproduces the one-chain
-    broadcast loop bit for bit: flags, proposal LLs and recorded rows."""
+    broadcast loop bit for bit: flags, proposal LLs and recorded rows; so does the opt-in
+    one-barrier step kernel (step.h, where it applies)."""
     from gpu_cases import run_engine
     fam, sizes, priors, pooling, names = synthetic(kind, C, G, N, ragged=ragged)
     P = fam.n_params
     st, _ = _synthetic_state(fam, sizes, priors, pooling, C, P, len(sizes))
     runs = {}
-    for rows in ("paired", "bcast"):
-        runs[rows] = run_engine(fam, sizes, st, numpy.arange(C), 5, n_iter, 777, pooling=pooling,
-                                priors=priors, env={"NMC_ROWS": rows}, tune_interval=7)
+    envs = {"paired": {"NMC_ROWS": "paired"}, "bcast": {"NMC_ROWS": "bcast"},
+            # the opt-in one-barrier step kernel (step.h), both variant flags
+            "step": {"NMC_STEP": "1", "NMC_STEP_FLAGS": "3"}}
+    for name, env in envs.items():
+        runs[name] = run_engine(fam, sizes, st, numpy.arange(C), 5, n_iter, 777, pooling=pooling,
+                                priors=priors, env=env, tune_interval=7)
     for k in range(3):
         assert numpy.array_equal(runs["paired"][k], runs["bcast"][k], equal_nan=True), k
+        assert numpy.array_equal(runs["paired"][k], runs["step"][k], equal_nan=True), k
     assert runs["paired"][0].mean() > 0.02

@@ -85,7 +85,11 @@ def test_cfg3_full_size_launch_modes_and_oracle(gpu_lib):
     assert not launch[3]["persistent"]
     bcast = _run(fam, sizes, st, sel, 0, n_iter, seed, env={"NMC_ROWS": "bcast"})
     assert bcast[3]["persistent"], bcast[3]
-    for other in (launch, bcast):
+    # the one-barrier step kernel (opt-in) in its two proposal / Gibbs-payload variants
+    step0 = _run(fam, sizes, st, sel, 0, n_iter, seed, env={"NMC_STEP": "1"})
+    step3 = _run(fam, sizes, st, sel, 0, n_iter, seed, env={"NMC_STEP": "1", "NMC_STEP_FLAGS": "3"})
+    assert step0[3]["kernel"].startswith("nmc_k_step<"), step0[3]
+    for other in (launch, bcast, step0, step3):
         for k in range(3):
             assert numpy.array_equal(pers[k], other[k], equal_nan=True), k
     acc = pers[0]

@@ -1,6 +1,7 @@
 #!/usr/bin/env python
 """Per-rank shard timings of the multi-GPU configs (diagnostics, not the contract
-bench): cfg 4 (1024 chains x 256 groups x 2000 obs over 8 GPUs -> 128 chains per rank,
+bench): cfg 2 (256 chains x 32 groups x 500 obs, Gaussian means, no pooling, one GPU),
+cfg 4 (1024 chains x 256 groups x 2000 obs over 8 GPUs -> 128 chains per rank,
 partial-pooling regression) and cfg 5 (512 x 128 x 5000 over 8 -> 64 chains per rank,
 8-parameter logistic, built-in family and the same model as a runtime-compiled user
 family)."""
@@ -19,18 +20,17 @@ LOGISTIC8 = r"""
 __device__ double nmc_user_loglik(const double* th, const double* row, const double* k) {
   double eta = th[0];
   for (int j = 0; j < 7; ++j) eta = fma(row[j], th[j + 1], eta);
-  double lae;
-  if (eta == 0.0) lae = NMC_LN2;
-  else lae = eta > 0.0 ? eta + log1p(exp(-eta)) : log1p(exp(eta));
-  return row[7] * eta - lae;
+  return row[7] * eta - nmc_logaddexp0(eta);
 }
 """
 
 
 def main():
-    which = sys.argv[1:] or ["cfg4", "cfg5", "cfg5user"]
+    which = sys.argv[1:] or ["cfg2", "cfg4", "cfg5", "cfg5user"]
     for w in which:
-        if w == "cfg4":
+        if w == "cfg2":     # example.distribution, none pooling, 256 x 32 x 500, one GPU
+            r = run("gauss", 256, 32, 500, "none", 0, 200)
+        elif w == "cfg4":
             r = run("linreg", 128, 256, 2000, "partial", 0, 40)
         elif w == "cfg4w4":   # four waves per workgroup: two workgroups per CU, resident
             r = run("linreg", 128, 256, 2000, "partial", 4, 40)
