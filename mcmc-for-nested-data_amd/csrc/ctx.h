@@ -56,7 +56,7 @@ struct nmc_ctx {
   int* gidx = nullptr;                    // [n_obs] group of each observation (obs-LL rows)
   int64_t nmax_group = 0;                 // rows of the largest group
   int split_batch = 0;                    // row split: chain blocks per (resident) launch
-  bool tmo_clean = false;                 // timeout flag read clear, no launch since
+  volatile unsigned* tmo_host = nullptr;  // host view of d.tmo (coherent pinned memory)
   void* user = nullptr;                   // user family: its per-device kernel table (user.hip)
   double* user_k = nullptr;               // user family: device copy of the model constants
   bool step_ok = false;                   // nmc_k_step where it applies (NMC_STEP=1)
@@ -74,7 +74,7 @@ static inline size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
              .total * 512;
 }
 static inline int run_mode(const nmc_ctx* x) {
-  if (x->pooling != NMC_POOL_PARTIAL) return NMC_MODE_NOPOOL;
+  if (x->pooling != NMC_POOL_PARTIAL) return x->d.CL == 32 ? NMC_MODE_HALF : NMC_MODE_NOPOOL;
   if (!x->persistent) return NMC_MODE_LAUNCH;
   if (x->d.hreg) return NMC_MODE_SYNC_REG;
   return x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;

@@ -93,13 +93,20 @@ struct Dev {
   int nmax;              // rows of the largest group
   int hlds, naux;        // persistent partial: Gibbs payload via LDS, auxiliary waves
   int hreg;              // persistent partial, G <= 64: Gibbs payload in registers (SYNC_REG)
+  // SYNC_REG with G > 64 ("owner" hand-off): the Gibbs update of task k (parameter k % P
+  // after iteration k / P) is computed once per chain block, by the Gibbs wave of the
+  // workgroup of group k % G (member 0), one step after its publication; it writes the
+  // hyper-parameters to the global slot and counts them on hrd[(cb * P + q) * 32]; every
+  // workgroup then reads the four values instead of streaming the G published values itself
+  int hown;
+  unsigned* hrd;         // [RB][P][32] hyper-ready counters (pbase tasks per parameter before)
   int noprio;            // diagnostics: no issue priority for the latency-bound waves
   int sflags;            // nmc_k_step variants (bit-identical; NMC_STEP_FLAGS): 1 Gibbs payload
                          // via LDS-DMA, 2 next proposal formed before the barrier
   int rows_lds;          // 1: each workgroup stages its group's rows in LDS once per launch
   int tile;              // target rows per likelihood tile (nmc_tiles)
   unsigned* cnt;         // [CB][P][32] publish counters (persistent partial), zeroed per launch
-  unsigned* tmo;         // timeout word (persists; host checks it)
+  unsigned* tmo;         // timeout word: pinned host memory, mapped (host reads it directly)
   // variates of iterations [vbase, vbase + vcap): filled by nmc_k_fill
   double* vzl;           // [t][P][G][C][2] {proposal normal, log accept uniform}
   double* vh;            // [t][P][C][2]    {hyper mean normal, hyper Gamma(a) draw}
@@ -506,10 +513,32 @@ __device__ __forceinline__ bool nmc_poll_published(const Dev& d, int cb, int p, 
     for (int k = 0; k < 8; ++k) tot += __builtin_amdgcn_readlane(v, k);
     if (tot >= target) return true;
     if ((spins & 255) == 255 &&
-        __hip_atomic_load(d.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+        __hip_atomic_load(d.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
       return false;
     if (spins >= NMC_SPIN_LIMIT) {
-      __hip_atomic_store(d.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// Owner hand-off (Dev.hown): the workgroup whose Gibbs wave computes task k, and the
+// calling wave's bounded poll of a task counter (the hyper-ready count of (cb, q)).
+__device__ __forceinline__ int nmc_task_owner(const Dev& d, int k) { return k % d.G; }
+__device__ __forceinline__ unsigned* nmc_hrd(const Dev& d, int cb, int q) {
+  return d.hrd + ((size_t)cb * d.P + q) * 32;
+}
+__device__ __forceinline__ bool nmc_poll_count(const Dev& d, const unsigned* ctr,
+                                               unsigned target) {
+  for (unsigned spins = 0;; ++spins) {
+    const unsigned v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v >= target) return true;
+    if ((spins & 255) == 255 &&
+        __hip_atomic_load(d.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+      return false;
+    if (spins >= NMC_SPIN_LIMIT) {
+      __hip_atomic_store(d.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
     }
     __builtin_amdgcn_s_sleep(2);
@@ -720,7 +749,10 @@ constexpr bool nmc_paired_rows_ok() {
   constexpr int R = (BD / NF) > 0 ? (BD / NF) : 1;
   return R % 2 == 0;
 }
-template <class Fam, bool PAIRED = false>
+// SAME (half layout): lanes l and l + 32 hold the same chain -- each evaluates its row
+// parity for that chain only, and the partner's own accumulators are this chain's other
+// parity (no partner evaluation).
+template <class Fam, bool PAIRED = false, bool SAME = false>
 __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename Fam::Reg& reg,
                                                 const double* __restrict__ p, int n,
                                                 double (&acc)[Fam::NACC],
@@ -752,7 +784,7 @@ __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename F
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int k = 0; k < Fam::NACC; ++k) u[s][k] = v[s][k] = 0.0;
-    if constexpr (Fam::ASM_ROWS) {
+    if constexpr (Fam::ASM_ROWS && !SAME) {
       static_assert(R == 8 && NF == 2, "the asm row loop is the 8-row {x, y} block");
       if (nb2 > 0)
         nmc_rows_lds_linreg2_paired(ph, nb2, reg.b0, reg.b[0], preg->b0, preg->b[0], u[0][0],
@@ -773,7 +805,7 @@ __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename F
 #pragma unroll
         for (int m = 0; m < RH; ++m) {
           fam.accum(reg, A + m * NF, u[m & 1]);
-          fam.accum(*preg, A + m * NF, v[m & 1]);
+          if constexpr (!SAME) fam.accum(*preg, A + m * NF, v[m & 1]);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -784,7 +816,7 @@ __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename F
 #pragma unroll
         for (int m = 0; m < RH; ++m) {
           fam.accum(reg, B + m * NF, u[m & 1]);
-          fam.accum(*preg, B + m * NF, v[m & 1]);
+          if constexpr (!SAME) fam.accum(*preg, B + m * NF, v[m & 1]);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -793,7 +825,9 @@ __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename F
     // partner chain is this lane's chain)
 #pragma unroll
     for (int k = 0; k < Fam::NACC; ++k) {
-      const nmc_pair2 e = nmc_halves(v[0][k]), o = nmc_halves(v[1][k]);
+      // (SAME: the other parity of this chain is the partner lane's own accumulators)
+      const nmc_pair2 e = nmc_halves(SAME ? u[0][k] : v[0][k]);
+      const nmc_pair2 o = nmc_halves(SAME ? u[1][k] : v[1][k]);
       const double p0 = h ? e.lo : e.hi, p1 = h ? o.lo : o.hi;
       a[0][k] = h ? p0 : u[0][k];
       a[1][k] = h ? u[0][k] : p0;
@@ -1111,10 +1145,11 @@ __device__ __forceinline__ void nmc_hyper_compute(const Dev& d, int cb, int t, i
   hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
   if (write && nmc_lane_owns(d, c, lane)) {
     const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
-    d.mu[ho] = mu;
-    d.s2[ho] = s2n;
-    d.hsd[ho] = sdn;
-    d.hlsd[ho] = lsd;
+    // write-through (sc1): the owner hand-off's readers poll for them inside the launch
+    __hip_atomic_store(d.mu + ho, mu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d.s2 + ho, s2n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d.hsd + ho, sdn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d.hlsd + ho, lsd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int row = nmc_record_row(d, t);
     if (row >= 0) {
       double* out = d.samples + ((size_t)row * d.cols + (size_t)p * (G + 2)) * C + c;
@@ -1216,10 +1251,11 @@ __device__ __forceinline__ void nmc_hyper_finish(const Dev& d, int cb, int t, in
   hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
   if (write && nmc_lane_owns(d, c, lane)) {
     const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
-    d.mu[ho] = mu;
-    d.s2[ho] = s2n;
-    d.hsd[ho] = sdn;
-    d.hlsd[ho] = lsd;
+    // write-through (sc1): the owner hand-off's readers poll for them inside the launch
+    __hip_atomic_store(d.mu + ho, mu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d.s2 + ho, s2n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d.hsd + ho, sdn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d.hlsd + ho, lsd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int row = nmc_record_row(d, t);
     if (row >= 0) {
       double* out = d.samples + ((size_t)row * d.cols + (size_t)p * (G + 2)) * C + c;
@@ -1270,10 +1306,10 @@ __device__ __forceinline__ void nmc_split_exchange(const Dev& d, int cb, int g, 
     const unsigned v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (v >= target) break;
     if ((spins & 255) == 255 &&
-        __hip_atomic_load(d.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+        __hip_atomic_load(d.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
       break;
     if (spins >= NMC_SPIN_LIMIT) {
-      __hip_atomic_store(d.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -1350,6 +1386,23 @@ __device__ __forceinline__ double nmc_pairwise_stream(const Dev& d, const double
   return ls[0];
 }
 
+// Owner hand-off: the hyper-parameters of task (tq, q) as its owner stored them (global
+// slot of tq, sc1 loads) -> this workgroup's LDS hyper state (nmc_hyper_finish's values).
+__device__ __forceinline__ void nmc_hyper_read(const Dev& d, int tq, int q, int cc, double* lds,
+                                               int hyp) {
+  const int lane = threadIdx.x & 63;
+  const int P = d.P;
+  const size_t ho = nmc_hslot(d, tq) + (size_t)q * d.C + cc;
+  const double mu = nmc_ldv<NMC_SRC_SC1>(d.mu + ho), s2 = nmc_ldv<NMC_SRC_SC1>(d.s2 + ho);
+  const double sd = nmc_ldv<NMC_SRC_SC1>(d.hsd + ho), lsd = nmc_ldv<NMC_SRC_SC1>(d.hlsd + ho);
+  double* hy = lds + hyp * 64 + lane;
+  hy[(NMC_HY_MU * P + q) * 64] = mu;
+  hy[(NMC_HY_SD * P + q) * 64] = sd;
+  hy[(NMC_HY_LSD * P + q) * 64] = lsd;
+  hy[(NMC_HY_S2 * P + q) * 64] = s2;
+  hy[(NMC_HY_ISD * P + q) * 64] = 1.0 / sd;
+}
+
 // The register Gibbs update of task (tq, q) for this wave's 64 chains: G <= 64 from one
 // 64-value fetch (nmc_hyper_fetch_reg / _compute_reg), 64 < G <= 256 streamed
 // (nmc_pairwise_stream, two passes).  Same sums, draws and outputs either way.
@@ -1400,15 +1453,23 @@ enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
        NMC_MODE_LAUNCH = 1,      // one launch per iteration, plain loads after the boundary
        NMC_MODE_SYNC = 2,        // persistent, sc1 loads after the barrier
        NMC_MODE_SYNC_LDS = 3,    // persistent, the Gibbs wave works on an LDS copy
-       NMC_MODE_SYNC_REG = 4 };  // persistent, G <= 64: the Gibbs wave fetches the task's
+       NMC_MODE_SYNC_REG = 4,    // persistent, G <= 64: the Gibbs wave fetches the task's
                                  // values straight into registers and updates in one step
+                                 // (G > 64: the owner hand-off, Dev.hown; 5 = its report)
+       NMC_MODE_HALF = 6 };      // none/complete pooling, 32 chains per workgroup: lanes l
+                                 // and l + 32 hold chain l, on the two row parities
 // RL: the groups' rows are staged in LDS for the launch (d.rows_lds) -- a template
 // parameter so each instance holds only its own row loop (the LDS-DMA staged loop's
 // registers raised the rows-in-LDS kernel's pressure: ~5 % of its time at cfg 3)
 template <class Fam, int MODE, bool RL = true>
 __global__ void __launch_bounds__(512)
 nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int flags) {
-  constexpr bool PARTIAL = MODE != NMC_MODE_NOPOOL;
+  constexpr bool PARTIAL = MODE != NMC_MODE_NOPOOL && MODE != NMC_MODE_HALF;
+  // half layout: the grid of 64-chain blocks would leave CUs idle (none/complete pooling,
+  // RB * G * 2 <= CUs): 32 chains per workgroup, twice the workgroups, each lane pair
+  // (l, l + 32) one chain with the paired row loop's two row parities -- the same rows,
+  // accumulators and order as the 64-chain layout, so every sum is bit-identical
+  constexpr bool HALF = MODE == NMC_MODE_HALF;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1418,8 +1479,9 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const int S = d.S;
   const int mb = b % S;                           // row-split member (S == 1: 0)
   const int g = (b / S) % G, cb = (b / S) / G + d.cb0;
-  const int c = nmc_lane_chain(d, cb, lane);
-  const bool live = nmc_lane_owns(d, c, lane) && mb == 0;   // member 0 writes the outputs
+  const int c = HALF ? cb * 32 + (lane & 31) : nmc_lane_chain(d, cb, lane);
+  // member 0 writes the outputs (half layout: lanes 0-31)
+  const bool live = nmc_lane_owns(d, c, lane) && mb == 0 && (!HALF || lane < 32);
   const bool g0w = g == 0 && mb == 0;   // writes the chain block's hyper-parameters
   const int cc = c < C ? c : C - 1;
   constexpr bool sync =
@@ -1556,7 +1618,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     const typename Fam::Reg reg = fam.prepare(thp);
     // paired rows: the partner lane's (lane ^ 32) proposal parameters
     typename Fam::Reg preg = reg;
-    if constexpr (nmc_paired_rows_ok<Fam>()) if (d.paired) {
+    if constexpr (nmc_paired_rows_ok<Fam>() && !HALF) if (d.paired) {
       const bool hi = lane >= 32;
 #pragma unroll
       for (int q = 0; q < Fam::MAXP; ++q) {
@@ -1583,10 +1645,11 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       double acc[Fam::NACC];
       if constexpr (RL) {
         bool done = false;
-        if constexpr (nmc_paired_rows_ok<Fam>()) if (d.paired) {
-          // two chains per lane, row pairs split by lane half
-          nmc_ll_rows_lds<Fam, true>(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc,
-                                     &preg);
+        if constexpr (nmc_paired_rows_ok<Fam>()) if (HALF || d.paired) {
+          // two chains per lane, row pairs split by lane half (half layout: one chain per
+          // lane pair, each lane its row parity)
+          nmc_ll_rows_lds<Fam, true, HALF>(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn,
+                                           acc, &preg);
           done = true;
         }
         if (!done)   // wave-uniform LDS address: broadcast ds_reads, pipelined
@@ -1609,6 +1672,77 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   // ---- register mode: the Gibbs wave runs its own loop, so its 64-value payload never
   //      shares registers with the control code; after its update it takes likelihood
   //      tiles like every other wave, and it meets them at the same two barriers ----
+  if constexpr (hr) if (gw && d.hown) {
+    // owner hand-off (G > 64): at step gs the wave (a) reads task gs - lag, computed by its
+    // owner, for this step's priors and (b) computes task gs - 1 when this workgroup owns
+    // it (needed at step gs - 1 + P); P == 1 needs task gs - 1 at once: (b) before (a)
+    const int gs0 = i0 * P;
+    const bool own = mb == 0;
+    auto owner_task = [&](int k) -> bool {   // poll the publication, update, count it
+      if (!own || k < gs0 || nmc_task_owner(d, k) != g) return true;
+      const int kq = k % P, kt = k / P;
+      if (!nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1))) return false;
+      // keep the payload loads below the poll (no instruction: wavefront scope)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      nmc_hyper_update_reg(d, cb, kt, kq, cc, lds, L.hyp, true);
+      nmc_drain_vm();   // the hyper-parameters are stored before they are counted
+      if (lane == 0)
+        __hip_atomic_fetch_add(nmc_hrd(d, cb, kq), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    };
+    for (int t = i0; t < i1 && ok; ++t) {
+      for (int p = 0; p < P; ++p) {
+        const int gs = t * P + p;
+        const bool due = gs - lag >= gs0;
+        bool okw = P == 1 ? owner_task(gs - 1) : true;
+        if (due) {   // task k = gs - lag = (kt, kq): wait for its owner, read it
+          const int k = gs - lag, kq = k % P, kt = k / P;
+          const bool r = okw && nmc_poll_count(d, nmc_hrd(d, cb, kq), (unsigned)(kt - i0 + 1) + d.pbase);
+          if (lane == 0)
+            __hip_atomic_store(lds + L.flag * 64 + 1, r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (r) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            nmc_hyper_read(d, kt, kq, cc, lds, L.hyp);
+            if (P <= 2) {   // this step's priors from the update just read
+              const int sp = gs & 1;
+              const double v = th[p * 64];
+              const double prop = v + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
+                                          lds[(L.zl + 2 * sp) * 64 + 2 * lane];
+              const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
+              const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
+              cwv[NMC_CW_LPC * 64] =
+                  t > 0 ? nmc_norm_logpdf_r(v, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
+              cwv[NMC_CW_LPP * 64] = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
+            }
+          }
+        }
+        // (a failed owner poll has set the timeout word: the next due poll fails and every
+        // wave leaves at the same step)
+        if (P > 1) okw = owner_task(gs - 1);
+        (void)okw;
+        __syncthreads();   // A
+        if (due) {
+          ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
+          if (!ok) break;
+        }
+        __syncthreads();   // B
+      }
+    }
+    // closing: the last task's owner computes and counts it (the matching barrier of the
+    // other waves' nmc_wait_published); every earlier task was computed in the loop
+    if (ok && own && nmc_task_owner(d, i1 * P - 1) == g) {
+      if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L)) {
+        nmc_hyper_update_reg(d, cb, i1 - 1, P - 1, cc, lds, L.hyp, true);
+        nmc_drain_vm();
+        if (lane == 0)
+          __hip_atomic_fetch_add(nmc_hrd(d, cb, P - 1), 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    nmc_drain_vm();
+    return;
+  }
   if constexpr (hr) if (gw) {
     const int gs0 = i0 * P;
     for (int t = i0; t < i1 && ok; ++t) {
@@ -1938,8 +2072,9 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     }
     d.ll[gc] = c_LL;
   }
-  // ---- closing Gibbs updates after i1-1 (group-0 workgroups write and record them) ----
-  if constexpr (hl) if (ok && g0w) {
+  // ---- closing Gibbs updates after i1-1 (group-0 workgroups write and record them; the
+  //      owner hand-off: the last task's owner) ----
+  if constexpr (hl) if (ok && (hr && d.hown ? mb == 0 && nmc_task_owner(d, i1 * P - 1) == g : g0w)) {
     const int ge = i1 * P;   // tasks ge-2 (copied at the last step; P >= 2) and ge-1 are left
     if (!hr && P >= 2 && gw) {
       const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 2)) * C + cc) * 2;

@@ -76,7 +76,7 @@ static void choose_geometry(nmc_ctx* x) {
   }
 #endif
   // partial pooling, persistent payload-in-LDS mode: wave 1 is the Gibbs wave
-  d.naux = x->pooling == NMC_POOL_PARTIAL && d.W >= 3 && d.G <= 256 ? 1 : 0;
+  d.naux = x->pooling == NMC_POOL_PARTIAL && d.W >= 3 && d.nleaf <= 4 ? 1 : 0;
   // rows in LDS when they fit beside the rest of the carve (64 KiB for the rows)
   d.rows_lds = (size_t)d.nmax * x->nf * 8 <= (size_t)64 * 1024 &&
                lds_bytes_for(x, 0, 1) <= (size_t)96 * 1024;
@@ -90,14 +90,18 @@ static void choose_geometry(nmc_ctx* x) {
   d.hlds = d.naux > 0 && d.G <= 128 && lds_bytes_for(x, 1, d.rows_lds) <= (size_t)160 * 1024 &&
            !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
   // G <= 64: the Gibbs wave fetches a task's values into registers (one sc1 round trip)
-  // and updates in the step after publication (no LDS payload, no two-stage pipeline)
-  // (NMC_HREG_STREAM=1, 64 < G <= 256: the values streamed through registers in 64-value
-  // chunks, two passes, nmc_pairwise_stream; measured 61 against 53 us/iter for the
-  // all-wave update at the cfg-4 shard -- one wave's four serial round trips per pass
-  // land on the step that needs the priors -- so opt-in)
-  const bool stream = getenv("NMC_HREG_STREAM") && atoi(getenv("NMC_HREG_STREAM"));
-  d.hreg = d.naux > 0 && (d.G <= 64 ? d.hlds : stream && d.nleaf <= 4) &&
+  // and updates in the step after publication (no LDS payload, no two-stage pipeline).
+  // 64 < G (at most 4 numpy leaves): the owner hand-off -- task k is updated once per chain
+  // block, by the Gibbs wave of group k % G's workgroup one step after publication (the
+  // values streamed through registers in 64-value chunks, two passes), and every other
+  // workgroup reads its four results (each workgroup streaming all G values itself measured
+  // 61 against 53 us/iter for the all-wave update at the cfg-4 shard).  NMC_NO_HOWN=1 keeps
+  // the all-wave / LDS-payload modes (bit-identical; tests compare them).
+  d.hown = d.naux > 0 && d.G > 64 && d.nleaf <= 4 &&
+           !(getenv("NMC_NO_HOWN") && atoi(getenv("NMC_NO_HOWN")));
+  d.hreg = d.naux > 0 && (d.G <= 64 ? d.hlds : d.hown) &&
            !(getenv("NMC_NO_HREG") && atoi(getenv("NMC_NO_HREG")));
+  if (!d.hreg) d.hown = 0;
   // Partial pooling whose grid is more than one 8-wave workgroup per CU but fits two
   // 4-wave ones (cfg-4 shards: 2 chain blocks x 256 groups): four waves, so the whole
   // grid is resident and runs persistent (both chain blocks' workgroups share each CU
@@ -116,11 +120,21 @@ static void choose_geometry(nmc_ctx* x) {
   // reads; NMC_ROWS=bcast keeps the one-chain broadcast loop (same sums bit for bit)
   d.paired = d.rows_lds && x->nf <= 4;
   if (const char* e = getenv("NMC_ROWS")) d.paired = d.paired && strcmp(e, "bcast") != 0;
+
   // nmc_k_step (one barrier per step, every wave deciding) measured slower than nmc_k_run
   // on MI355X (cfg 3: 8.8 against 8.0 us/iter, profiles/r03_step_kernel_ab.json): opt-in,
   // NMC_STEP=1, bit-identical (tests/test_gpu_scale.py)
   x->step_ok = getenv("NMC_STEP") && atoi(getenv("NMC_STEP")) != 0;
   d.sflags = getenv("NMC_STEP_FLAGS") ? atoi(getenv("NMC_STEP_FLAGS")) : 0;
+  // none/complete pooling whose 64-chain grid fills at most half the CUs (cfg 2: 4 chain
+  // blocks x 32 groups on 256 CUs): 32 chains per workgroup, each lane pair one chain on
+  // the paired loop's two row parities (NMC_MODE_HALF) -- twice the workgroups, the same
+  // sums bit for bit.  NMC_HALF=0 keeps 64 chains per workgroup (tests compare them).
+  if (x->pooling != NMC_POOL_PARTIAL && d.S == 1 && d.paired && !x->step_ok &&
+      (int64_t)d.RB * d.G * 2 <= x->ncu && !(getenv("NMC_HALF") && !atoi(getenv("NMC_HALF")))) {
+    d.CL = 32;
+    d.RB = (d.C + d.CL - 1) / d.CL;
+  }
 }
 
 // numpy's pairwise-sum recursion over G groups (numpy/_core/src/umath/loops_utils.h):
@@ -160,11 +174,15 @@ static size_t cnt_bytes(const nmc_ctx* x) {
   return (size_t)32 * 8 * ((x->C + 31) / 32) * x->P * sizeof(unsigned);
 }
 
+// The timeout word lives in coherent pinned host memory mapped into the device: the
+// kernels' (rare) system-scope store lands in host memory, so the host reads it with a
+// plain load after a synchronize -- no device-to-host copy on every synchronize.
+// owner hand-off hyper-ready counters [RB <= ceil(C / 32)][P][32]
+static size_t hrd_words(const nmc_ctx* x) { return (size_t)32 * ((x->C + 31) / 32) * x->P; }
+
 static int check_timeout(nmc_ctx* x) {
-  unsigned t = 0;
-  HIPCHK(hipMemcpy(&t, x->d.tmo, sizeof(t), hipMemcpyDeviceToHost));
-  if (t) return fail(-5, "persistent kernel: a chain-block wait timed out (workgroups not resident?)");
-  x->tmo_clean = true;   // no launch since this check (nmc_run skips its own)
+  if (*x->tmo_host)
+    return fail(-5, "persistent kernel: a chain-block wait timed out (workgroups not resident?)");
   return 0;
 }
 
@@ -299,16 +317,29 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   rc |= dalloc(x, &dmerge, merges.size());
   // [RB][P][8 shards][32], RB <= ceil(C / 32)
   rc |= dalloc(x, &d.cnt, cnt_bytes(x) / sizeof(unsigned));
-  rc |= dalloc(x, &d.tmo, 4);
+  rc |= dalloc(x, &d.hrd, hrd_words(x));
   if (rc) { nmc_destroy(x); return rc; }
+  {
+    void* h = nullptr;
+    void* dp = nullptr;
+    e = hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess) x->tmo_host = (volatile unsigned*)h;
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&dp, h, 0);
+    if (e != hipSuccess) {
+      nmc_destroy(x);
+      return fail(-2, std::string("timeout word (pinned host memory): ") + hipGetErrorString(e));
+    }
+    memset(h, 0, 64);
+    d.tmo = (unsigned*)dp;
+  }
   HIPCHK(hipMemset(d.cnt, 0, cnt_bytes(x)));
+  HIPCHK(hipMemset(d.hrd, 0, hrd_words(x) * sizeof(unsigned)));
   d.pbase = d.xbase = 0;
   d.leaf = dleaf;
   d.merge = dmerge;
   HIPCHK(hipMemcpy(dleaf, starts.data(), starts.size() * sizeof(int), hipMemcpyHostToDevice));
   if (!merges.empty())
     HIPCHK(hipMemcpy(dmerge, merges.data(), merges.size() * sizeof(int), hipMemcpyHostToDevice));
-  HIPCHK(hipMemset(d.tmo, 0, 16));
   int64_t nmax = 0;
   for (int g = 0; g < n_groups; ++g)
     nmax = std::max<int64_t>(nmax, group_offsets[g + 1] - group_offsets[g]);
@@ -404,6 +435,7 @@ int nmc_destroy(nmc_ctx* x) {
   for (auto& pr : x->kev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   for (auto& pr : x->hev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   if (x->stream) hipStreamDestroy(x->stream);
+  if (x->tmo_host) hipHostFree((void*)x->tmo_host);
   delete x;
   return 0;
 }
@@ -545,12 +577,8 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
   if (iter_begin == iter_end) return 0;
   if (x->rng == NMC_RNG_REPLAY && (!x->d.rz || iter_end > x->d.replay_n))
     return fail(-1, "replay variates do not cover the iteration range");
-  if (!x->tmo_clean) {   // a persistent launch that already timed out: stop before queueing
-    unsigned t = 0;     // more work (a synchronous read: skipped right after a synchronize)
-    if (hipMemcpy(&t, x->d.tmo, sizeof(t), hipMemcpyDeviceToHost) == hipSuccess && t)
-      return check_timeout(x);
-  }
-  x->tmo_clean = false;
+  // a persistent launch that already timed out: stop before queueing more work
+  if (int rc0 = check_timeout(x)) return rc0;
   const bool partial = x->pooling == NMC_POOL_PARTIAL;
   const int P = x->P;
   // the kernels read the values after iteration iter_begin-1 from vb[(iter_begin-1)&1]
@@ -594,6 +622,7 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       if ((uint64_t)x->G * (x->d.pbase + (uint64_t)(c1 - c0)) >= (1ull << 31) ||
           (uint64_t)x->d.S * (x->d.xbase + steps) >= (1ull << 31)) {
         HIPCHK(hipMemsetAsync(x->d.cnt, 0, cnt_bytes(x), x->stream));
+        HIPCHK(hipMemsetAsync(x->d.hrd, 0, hrd_words(x) * sizeof(unsigned), x->stream));
         if (x->d.xcnt)
           HIPCHK(hipMemsetAsync(x->d.xcnt, 0, (size_t)x->d.RB * x->d.G * 32 * sizeof(unsigned),
                                 x->stream));
@@ -755,7 +784,8 @@ int nmc_split_config(nmc_ctx* x, int* members, int* chain_blocks_per_launch) {
 
 int nmc_kernel_name(nmc_ctx* x, char* out, int cap) {
   static const char* const modes[] = {"NMC_MODE_NOPOOL", "NMC_MODE_LAUNCH", "NMC_MODE_SYNC",
-                                      "NMC_MODE_SYNC_LDS", "NMC_MODE_SYNC_REG"};
+                                      "NMC_MODE_SYNC_LDS", "NMC_MODE_SYNC_REG", "",
+                                      "NMC_MODE_HALF"};
   const int mode = run_mode(x);
   std::string fam;
   switch (x->family) {
@@ -779,7 +809,9 @@ int nmc_launch_config(nmc_ctx* x, int* waves_per_group, int* chain_blocks, int* 
   *chain_blocks = x->d.RB;
   if (persistent) *persistent = x->persistent || x->pooling != NMC_POOL_PARTIAL ? 1 : 0;
   if (chains_per_block) *chains_per_block = x->d.CL;
-  if (mode) *mode = run_mode(x);
+  // (5: the register mode with the owner hand-off, G > 64 -- reported only; the kernel
+  // instance is the SYNC_REG one)
+  if (mode) *mode = run_mode(x) == NMC_MODE_SYNC_REG && x->d.hown ? 5 : run_mode(x);
   return 0;
 }
 

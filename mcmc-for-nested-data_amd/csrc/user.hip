@@ -26,7 +26,7 @@ namespace {
 // (nmc_k_run: mode m with rows in LDS at UK_RUN0 + m, rows staged at UK_RUN0 + 5 + m;
 // nmc_k_step: NOPOOL / SYNC_REG at UK_STEP0 / UK_STEP0 + 1)
 enum { UK_RUN0 = 0, UK_NRUN = 5, UK_GROUP_LL = 10, UK_OBS_LL_ROWS = 11, UK_OBS_LL = 12,
-       UK_STEP0 = 13, UK_GROUP_LL_RL = 15, UK_GROUP_FIN = 16, UK_N = 17 };
+       UK_STEP0 = 13, UK_GROUP_LL_RL = 15, UK_GROUP_FIN = 16, UK_HALF = 17, UK_N = 18 };
 const char* const kNames[UK_N] = {
     "nmc_k_run<FamUser, 0, true>", "nmc_k_run<FamUser, 1, true>", "nmc_k_run<FamUser, 2, true>",
     "nmc_k_run<FamUser, 3, true>", "nmc_k_run<FamUser, 4, true>",
@@ -34,9 +34,11 @@ const char* const kNames[UK_N] = {
     "nmc_k_run<FamUser, 2, false>", "nmc_k_run<FamUser, 3, false>",
     "nmc_k_run<FamUser, 4, false>", "nmc_k_group_part<FamUser, false>", "nmc_k_obs_ll_rows<FamUser>",
     "nmc_k_obs_ll<FamUser>", "nmc_k_step<FamUser, 0>", "nmc_k_step<FamUser, 4>",
-    "nmc_k_group_part<FamUser, true>", "nmc_k_group_fin<FamUser>"};
+    "nmc_k_group_part<FamUser, true>", "nmc_k_group_fin<FamUser>",
+    "nmc_k_run<FamUser, 6, true>"};
 int run_index(const nmc_ctx* x, int mode) {
   if (uses_step(x, mode)) return UK_STEP0 + (mode == NMC_MODE_NOPOOL ? 0 : 1);
+  if (mode == NMC_MODE_HALF) return UK_HALF;
   return UK_RUN0 + mode + (x->d.rows_lds ? 0 : UK_NRUN);
 }
 
@@ -194,7 +196,7 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
       const int e = nmc_run_launches(x, i0, i1, [&](int mode, const Dev& d, dim3 grid,
                                                    dim3 block, size_t lds) {
         if (rc) return;
-        if (mode < 0 || mode >= UK_NRUN) {
+        if (mode < 0 || (mode >= UK_NRUN && mode != NMC_MODE_HALF)) {
           rc = nmc_fail(-1, "user family: unknown step-kernel mode");
           return;
         }

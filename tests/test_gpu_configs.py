@@ -49,20 +49,23 @@ def test_cfg4_geometry_multileaf_gibbs(gpu_lib, G):
     # one chain block: G workgroups, co-resident -> persistent (SYNC, multi-leaf plan)
     one = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed)
     assert one[3]["persistent"], one[3]
-    # the same chains in a two-block launch (two 4-wave workgroups per CU, persistent) and
+    assert one[3]["mode"] == "NMC_MODE_SYNC_OWN", one[3]
+    # the same chains in a two-block launch (two 4-wave workgroups per CU, persistent, the
+    # owner hand-off: task k updated once per chain block by group k % G's Gibbs wave) and
     # forced launch per iteration
     two = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed)
     lau = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, env={"NMC_PERSIST": "0"})
     assert not lau[3]["persistent"]
-    # the register hand-off with the values streamed in 64-value chunks (opt-in)
-    reg = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed,
-                     env={"NMC_HREG_STREAM": "1"})
-    if G == 256:   # (G = 129: 258 workgroups of > 80 KB LDS -> launch per iteration)
-        assert reg[3]["mode"] == "NMC_MODE_SYNC_REG", reg[3]
+    # the all-wave (G > 128) / LDS-payload (G <= 128) persistent modes, no owner hand-off
+    alw = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, env={"NMC_NO_HOWN": "1"})
+    assert alw[3]["mode"] != "NMC_MODE_SYNC_OWN", alw[3]
+    # launches of 3, 3 and 2 iterations (each launch's closing task, counters carried over)
+    spl = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, launch_iters=3)
     for k in range(3):
         assert numpy.array_equal(one[k], two[k][:64], equal_nan=True), k
         assert numpy.array_equal(two[k], lau[k], equal_nan=True), k
-        assert numpy.array_equal(two[k], reg[k], equal_nan=True), k
+        assert numpy.array_equal(two[k], alw[k], equal_nan=True), k
+        assert numpy.array_equal(two[k], spl[k], equal_nan=True), k
     assert 0.05 < lau[0].mean() < 0.95
     # chains 0, 1 and 127 against the oracle
     sel = numpy.array([0, 1, 127])
@@ -182,3 +185,30 @@ def test_rccl_gather_one_rank(gpu_lib):
         eng.close()
     finally:
         parallel.rccl_destroy(comm)
+
+
+def test_cfg2_full_size_half_layout(gpu_lib):
+    """cfg 2 (example/distribution.py:18-24 at 256 chains x 32 groups x 500 obs, no
+    pooling): the 64-chain grid is 128 workgroups on 256 CUs, so the step kernel runs the
+    half layout (32 chains per workgroup, NMC_MODE_HALF); flags, proposal LLs and recorded
+    rows are bit-identical to the 64-chain layout, and chains 0, 1 and 255 match the oracle."""
+    from gpu_cases import synthetic
+    C, G, N, n_iter, seed = 256, 32, 500, 6, 13
+    fam, sizes, priors, pooling, _ = synthetic("gauss_none", C, G, N)
+    r = numpy.random.RandomState(4)
+    from oracle import restatement as rs
+    nested = rs.Nested(fam, sizes)
+    value = numpy.repeat((r.normal(0, 0.3, size=(C, 3)))[:, :, None], G, axis=2)
+    lp = numpy.stack([numpy.asarray(priors[p].logpdf(value[:, p, :])) for p in range(3)], 1)
+    st = rs.State(value, lp, numpy.full((C, G), numpy.nan))
+    half = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, pooling=pooling,
+                      priors=priors)
+    full = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, pooling=pooling,
+                      priors=priors, env={"NMC_HALF": "0"})
+    assert half[3]["mode"] == "NMC_MODE_HALF" and half[3]["chains_per_block"] == 32, half[3]
+    assert full[3]["mode"] == "NMC_MODE_NOPOOL", full[3]
+    for k in range(3):
+        assert numpy.array_equal(half[k], full[k], equal_nan=True), k
+    assert 0.05 < half[0].mean() < 0.95
+    sel = numpy.array([0, 1, 255])
+    _check_vs_oracle(half, nested, st, sel, sel, n_iter, seed, pooling=pooling, priors=priors)

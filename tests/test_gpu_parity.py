@@ -201,12 +201,19 @@ def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
     st, _ = _synthetic_state(fam, sizes, priors, pooling, C, P, len(sizes))
     runs = {}
     envs = {"paired": {"NMC_ROWS": "paired"}, "bcast": {"NMC_ROWS": "bcast"},
+            # none pooling on few workgroups runs the half layout (32 chains per workgroup,
+            # lane pairs on the two row parities); this keeps 64 chains per workgroup
+            "full": {"NMC_HALF": "0"},
             # the opt-in one-barrier step kernel (step.h), both variant flags
             "step": {"NMC_STEP": "1", "NMC_STEP_FLAGS": "3"}}
     for name, env in envs.items():
         runs[name] = run_engine(fam, sizes, st, numpy.arange(C), 5, n_iter, 777, pooling=pooling,
                                 priors=priors, env=env, tune_interval=7)
+    if pooling != "partial":
+        assert runs["paired"][3]["mode"] == "NMC_MODE_HALF", runs["paired"][3]
+        assert runs["full"][3]["mode"] == "NMC_MODE_NOPOOL", runs["full"][3]
     for k in range(3):
         assert numpy.array_equal(runs["paired"][k], runs["bcast"][k], equal_nan=True), k
         assert numpy.array_equal(runs["paired"][k], runs["step"][k], equal_nan=True), k
+        assert numpy.array_equal(runs["paired"][k], runs["full"][k], equal_nan=True), k
     assert runs["paired"][0].mean() > 0.02

@@ -31,6 +31,10 @@ echo "== rocprof $(date +%T)" && \
     python3 "$ROOT/bench.py" --steps 20 --warmup 5 --cpu-seconds 0 --no-pmc \
     > "$ROOT/gpurun_out/bench_prof_$TAG.json" 2> "$ROOT/gpurun_out/bench_prof_$TAG.err") && \
 find gpurun_out/prof_$TAG -name "*stats*" && \
-echo "== fp64peak $(date +%T)" && \
-timeout -k 10 120 ./tools/fp64peak > gpurun_out/fp64peak_$TAG.jsonl 2>&1 && \
+echo "== launchcost $(date +%T)" && \
+timeout -k 10 200 python3 tools/launchcost.py > gpurun_out/launchcost_$TAG.json 2>&1 && \
+cut -c1-600 gpurun_out/launchcost_$TAG.json && \
+echo "== cfgbench $(date +%T)" && \
+timeout -k 10 300 python3 tools/cfgbench.py cfg2 cfg4 cfg5 > gpurun_out/cfgbench_$TAG.jsonl 2>&1 && \
+cut -c1-400 gpurun_out/cfgbench_$TAG.jsonl && \
 echo "== done $(date +%T)"
