@@ -165,7 +165,15 @@ struct Dev {
       if (e) d.stamps[512 + (si_ * 16 + (k)) * 4 + 2] = (unsigned long long)w;           \
     }                                                                                     \
   } while (0)
+// every workgroup b: stamps[1024 + b * 4 + {entry, prologue done, loop done, exit}],
+// s_memrealtime (100 MHz, one clock for the whole chip; tools/launchtl.py)
+#define NMC_RUN_SL(slot)                                                                  \
+  do {                                                                                    \
+    if (d.stamps && threadIdx.x == 0)                                                     \
+      d.stamps[1024 + (size_t)blockIdx.x * 4 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
+#define NMC_RUN_SL(slot) do {} while (0)
 #define NMC_TILE_STAMP(k, e) do {} while (0)
 #define NMC_STAMP_CMP(t, slot) do {} while (0)
 #define NMC_STAMP_AUX(t, slot) do {} while (0)
@@ -1470,6 +1478,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   // (l, l + 32) one chain with the paired row loop's two row parities -- the same rows,
   // accumulators and order as the 64-chain layout, so every sum is bit-identical
   constexpr bool HALF = MODE == NMC_MODE_HALF;
+  NMC_RUN_SL(0);
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1494,6 +1503,11 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   // counter add, poll -- is behind a whole step) and the priors that need it come from
   // the Gibbs wave when it lands in the step that uses it (P <= 2)
   const int lag = hr && P >= 2 ? 2 : 1;
+  // register mode: the task this workgroup closes after the loop (-1: none)
+  const int close_k = [&]() {
+    const int ge = i1 * P, k0 = ge - lag > i0 * P ? ge - lag : i0 * P;
+    return hr && mb == 0 && k0 + g < ge ? k0 + g : -1;
+  }();
   // rows in LDS for the launch, or every wave's two staging buffers (nmc_ll_rows_staged)
   const int row_doubles = RL ? d.nmax * Fam::NFIELDS
                              : (Fam::NFIELDS <= 4 ? 0 : nmc_stage_doubles(Fam::NFIELDS, blockDim.x >> 6));
@@ -1566,6 +1580,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     lds[L.flag * 64 + lane] = 0.0;       // (also zeroes both tile counters)
   }
   __syncthreads();
+  NMC_RUN_SL(1);
 
   bool ok = true;
   int pub_p = -1;     // control wave: parameter whose sc1 value store awaits its counter add
@@ -1782,15 +1797,13 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         __syncthreads();   // B
       }
     }
-    // closing: tasks ge-lag .. ge-1 (group-0 workgroups write and record them); the same
+    // closing: tasks ge-lag .. ge-1, task ge-lag+j by the workgroup of group j (member 0),
+    // which writes and records it -- in parallel, not one after the other; the same
     // barrier as the other waves' nmc_wait_published
-    if (ok && g0w) {
-      const int ge = i1 * P;
-      if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L)) {
-        for (int k = ge - lag > gs0 ? ge - lag : gs0; k < ge; ++k) {
-          nmc_hyper_update_reg(d, cb, k / P, k % P, cc, lds, L.hyp, true);
-        }
-      }
+    if (ok && close_k >= 0) {
+      if (nmc_wait_published(d, cb, close_k % P, (unsigned)G * (unsigned)(close_k / P - i0 + 1),
+                             lds, L))
+        nmc_hyper_update_reg(d, cb, close_k / P, close_k % P, cc, lds, L.hyp, true);
     }
     nmc_drain_vm();
     return;
@@ -2050,6 +2063,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     NMC_STAMP(t, 7);
   }
 
+  NMC_RUN_SL(2);
   if constexpr (sync) if (ctl && pub_p >= 0) {   // the last parameter's count
     nmc_drain_vm();
     if (lane == 0)
@@ -2074,7 +2088,9 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   }
   // ---- closing Gibbs updates after i1-1 (group-0 workgroups write and record them; the
   //      owner hand-off: the last task's owner) ----
-  if constexpr (hl) if (ok && (hr && d.hown ? mb == 0 && nmc_task_owner(d, i1 * P - 1) == g : g0w)) {
+  if constexpr (hl) if (ok && (hr ? (d.hown ? mb == 0 && nmc_task_owner(d, i1 * P - 1) == g
+                                           : close_k >= 0)
+                                  : g0w)) {
     const int ge = i1 * P;   // tasks ge-2 (copied at the last step; P >= 2) and ge-1 are left
     if (!hr && P >= 2 && gw) {
       const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 2)) * C + cc) * 2;
@@ -2082,7 +2098,9 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
                         ((ge - 2) & 1) * (G + 1));
     }
     // (register mode: the Gibbs wave closes in its own loop; this is the matching barrier)
-    const bool pub = nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L);
+    const int wk = hr && !d.hown ? close_k : ge - 1;   // the task whose publication is awaited
+    const bool pub = nmc_wait_published(d, cb, wk % P, (unsigned)G * (unsigned)(wk / P - i0 + 1),
+                                        lds, L);
     if (!hr && pub && gw) {
       const double* src = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
       const int ho = ((ge - 1) & 1) * (G + 1);
@@ -2104,6 +2122,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L))
       nmc_hyper<NMC_SRC_SC1>(d, ((i1 - 1) & 1) ? d.vb1 : d.vb0, cb, i1 - 1, lds, L, true);
   }
+  NMC_RUN_SL(3);
 }
 
 // Group log-likelihoods for arbitrary theta [P][G][C] (the batched start-point search and

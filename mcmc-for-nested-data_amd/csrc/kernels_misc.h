@@ -6,14 +6,18 @@
 
 // ---------------------------------------------------------------------------
 // Variates for iterations [iter0, iter0 + T): one thread per (t, p, g, c) element
-// of the step variates and per (t, p, c) of the hyper variates.
+// of the step variates and per (t, p, c) of the hyper variates.  The hyper variates come
+// first in the index space: their Gamma draws (rejection loops) are the longest threads,
+// and started first they run under the bulk of the step variates instead of after it.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) nmc_k_fill(Dev d, int iter0, int T) {
   const size_t PGC = (size_t)d.P * d.G * d.C, PC = (size_t)d.P * d.C;
   const size_t n1 = (size_t)T * PGC;
   const size_t n2 = d.pooling == NMC_POOL_PARTIAL ? (size_t)T * PC : 0;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n1 + n2;
-       i += (size_t)gridDim.x * blockDim.x) {
+  for (size_t i0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i0 < n1 + n2;
+       i0 += (size_t)gridDim.x * blockDim.x) {
+    // i0 < n2: hyper element i0; else step element i0 - n2
+    const size_t i = i0 < n2 ? n1 + i0 : i0 - n2;
     if (i < n1) {
       const int t = (int)(i / PGC);
       const size_t r = i % PGC;

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <charconv>
+#include <chrono>
 #include <string>
 #include <thread>
 #include <utility>
@@ -91,14 +92,16 @@ static void choose_geometry(nmc_ctx* x) {
            !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
   // G <= 64: the Gibbs wave fetches a task's values into registers (one sc1 round trip)
   // and updates in the step after publication (no LDS payload, no two-stage pipeline).
-  // 64 < G (at most 4 numpy leaves): the owner hand-off -- task k is updated once per chain
-  // block, by the Gibbs wave of group k % G's workgroup one step after publication (the
-  // values streamed through registers in 64-value chunks, two passes), and every other
-  // workgroup reads its four results (each workgroup streaming all G values itself measured
-  // 61 against 53 us/iter for the all-wave update at the cfg-4 shard).  NMC_NO_HOWN=1 keeps
-  // the all-wave / LDS-payload modes (bit-identical; tests compare them).
+  // 64 < G (at most 4 numpy leaves), opt-in NMC_HOWN=1: the owner hand-off -- task k is
+  // updated once per chain block, by the Gibbs wave of group k % G's workgroup one step
+  // after publication (the values streamed through registers in 64-value chunks, two
+  // passes), and every other workgroup reads its four results.  Bit-identical, but measured
+  // slower than the all-wave (G > 128) / LDS-payload (G <= 128) updates: 62 against 53
+  // us/iter at the cfg-4 shard, 1917 against 1654 us/iter at the cfg-5 shard -- the owner
+  // polls a task one step after its publication (a chain-block-wide wait every step) and
+  // its workgroup's barrier waits for the two streamed passes.
   d.hown = d.naux > 0 && d.G > 64 && d.nleaf <= 4 &&
-           !(getenv("NMC_NO_HOWN") && atoi(getenv("NMC_NO_HOWN")));
+           getenv("NMC_HOWN") && atoi(getenv("NMC_HOWN"));
   d.hreg = d.naux > 0 && (d.G <= 64 ? d.hlds : d.hown) &&
            !(getenv("NMC_NO_HREG") && atoi(getenv("NMC_NO_HREG")));
   if (!d.hreg) d.hown = 0;
@@ -647,9 +650,21 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
   return rc;
 }
 
+// Wait for the context's stream by polling it (hipStreamQuery) for up to 50 ms, then
+// blocking: the blocking wait's wake-up costs ~10 us per call (profiles/r03_launchcost:
+// wall minus event time), a tenth of a 20-iteration run.
 int nmc_synchronize(nmc_ctx* x) {
   hipSetDevice(x->device);
-  HIPCHK(hipStreamSynchronize(x->stream));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(x->stream);
+    if (e == hipSuccess) break;
+    if (e != hipErrorNotReady) return fail(-2, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+      HIPCHK(hipStreamSynchronize(x->stream));
+      break;
+    }
+  }
   return check_timeout(x);
 }
 

@@ -36,7 +36,7 @@ def _state(fam, sizes, C, P, seed=11):
     return rs.State(value, lp, ll, mu, s2), nested
 
 
-def _run(fam, sizes, st, sel, chain_base, n_iter, seed, env=None):
+def _run(fam, sizes, st, sel, chain_base, n_iter, seed, env=None, launch_iters=0):
     old = {}
     for k, v in (env or {}).items():
         old[k] = os.environ.get(k)
@@ -52,6 +52,8 @@ def _run(fam, sizes, st, sel, chain_base, n_iter, seed, env=None):
     eng.set_state(st.value[sel], st.lp[sel], st.ll[sel], st.mu[sel], st.s2[sel])
     eng.set_schedule(n_iter, n_iter // 2, 1, tune_interval=5)
     eng.set_trace(True)
+    if launch_iters:
+        eng.set_launch_iters(launch_iters)
     eng.run(0, n_iter)
     acc, llp = eng.trace(n_iter)
     rows = eng.samples()
@@ -85,11 +87,15 @@ def test_cfg3_full_size_launch_modes_and_oracle(gpu_lib):
     assert not launch[3]["persistent"]
     bcast = _run(fam, sizes, st, sel, 0, n_iter, seed, env={"NMC_ROWS": "bcast"})
     assert bcast[3]["persistent"], bcast[3]
+    # persistent launches of 5, 5 and 2 iterations: each launch's closing Gibbs tasks (one
+    # per closing workgroup, in parallel) and the publish counters carried over
+    multi = _run(fam, sizes, st, sel, 0, n_iter, seed, launch_iters=5)
+    assert multi[3]["mode"] == "NMC_MODE_SYNC_REG", multi[3]
     # the one-barrier step kernel (opt-in) in its two proposal / Gibbs-payload variants
     step0 = _run(fam, sizes, st, sel, 0, n_iter, seed, env={"NMC_STEP": "1"})
     step3 = _run(fam, sizes, st, sel, 0, n_iter, seed, env={"NMC_STEP": "1", "NMC_STEP_FLAGS": "3"})
     assert step0[3]["kernel"].startswith("nmc_k_step<"), step0[3]
-    for other in (launch, bcast, step0, step3):
+    for other in (launch, bcast, multi, step0, step3):
         for k in range(3):
             assert numpy.array_equal(pers[k], other[k], equal_nan=True), k
     acc = pers[0]
