@@ -1,41 +1,39 @@
 // kernels.h -- the MCMC sampling kernels for gfx950 (CDNA4, wave64, fp64).
 //
 // Layout: chain-on-lane.  A workgroup owns one (chain block of 64 chains, group g)
-// pair; its W waves split the group's CSR rows obs[off[g]..off[g+1]).  Every lane of
-// a wave holds ONE chain's parameters in registers while the whole wave walks the
-// same rows, so a row is read with a wave-uniform scalar load (s_load, SGPR operands)
-// and feeds 64 chains -- the cross-chain reuse that makes the dataset cache-resident.
+// pair (none/complete pooling on few workgroups: 32 chains, NMC_MODE_HALF); its W waves
+// split the group's CSR rows obs[off[g]..off[g+1]), staged once per launch in LDS.
+// Every lane holds one chain's parameters in registers while the wave walks the same
+// rows, so one broadcast ds_read feeds 64 chains (the paired loop: two chains per lane,
+// one row pair per read) -- the cross-chain reuse that keeps the dataset on chip.
 //
 // nmc_k_run runs the reference's Sampler._loop body (posteriorSampling.py:872-891)
 // for iterations [i0, i1) of every (chain, group).  Per parameter step p
 // (StepMethod.step :594-613):
 //   1. every wave proposes theta_p' = theta_p + scale*z (Parameter.propose :304-306)
-//      and accumulates the family log-likelihood over its row slice (:615-635);
-//   2. partial sums go to LDS (double-buffered by step parity), ONE barrier;
-//   3. every wave sums the W partials in the same fixed order and runs the identical
-//      Metropolis decision (:334-383, branch order exact, IEEE isfinite), tuning
-//      (:385-437) and group-LL propagation (:608-610) -- redundantly, so no second
-//      barrier is needed to broadcast the result.  Wave 0 alone writes outputs.
-// Per-(p, chain) state that changes (scale, log prior, counters) lives in LDS,
-// double-buffered by iteration parity; the current values live in one LDS column per
-// parameter (every wave writes the same value, so each wave sees its own write), the
-// group LL in a register.
+//      and takes likelihood row tiles of the group from an LDS queue (:615-635); the
+//      tile partition depends on the rows alone, so every sum is fixed;
+//   2. barrier A: the control wave (wave 0) adds the tile partials in a fixed order and
+//      makes the Metropolis decision (:334-383, branch order exact, IEEE isfinite),
+//      tuning (:385-437) and group-LL propagation (:608-610);
+//   3. barrier B: the decided value is visible; the rest of the state update is
+//      deferred into the next step's slack.
+// The step's {z, log u} are drawn by a job in the previous step's tile queue (Philox,
+// or the replayed reference variates).
 //
 // Partial pooling couples the G groups of a chain through the Gibbs update of the
-// hyper-parameters (HyperParameter.update :463-498).  Its update after iteration t-1
-// is only needed by the Metropolis decisions of iteration t (the prior of each
-// parameter), not by the likelihood.  So the update is computed right after the
-// step-0 likelihood of iteration t, redundantly by every workgroup of the chain
-// block, in numpy's pairwise-sum order (exact mean/variance parity):
-//   * persistent mode (every workgroup resident): values are published write-through
-//     (sc1 stores, vmcnt drain, one agent-scope counter add per workgroup and
-//     iteration); a workgroup waits for its chain block's counter only AFTER its
-//     step-0 likelihood, so the hand-off latency hides behind compute, and reads the
-//     published values with sc1 loads (MI355X_MICROARCH.md, inter-workgroup
-//     visibility: sc1 stores + counter + sc1 loads, no fences);
-//   * launch-per-iteration mode (grid too large to be resident): the kernel
-//     boundary publishes, plain loads read.
-// Every spin is bounded: a timeout sets d.tmo and every workgroup drains.
+// hyper-parameters (HyperParameter.update :463-498).  The update of parameter q after
+// iteration t is needed first by the decision of step (t + 1, q), not by any
+// likelihood, so it is pipelined behind the steps in between:
+//   * persistent modes (every workgroup resident): decided values are published
+//     write-through (sc1 stores, vmcnt drain, one agent-scope counter add per
+//     workgroup and step); the Gibbs wave (wave 1) polls the chain block's counter two
+//     steps later, reads the values with sc1 loads (MI355X_MICROARCH.md, inter-workgroup
+//     visibility) and updates in numpy's pairwise order (exact mean/variance parity);
+//   * launch-per-iteration mode (grid too large to be resident): the kernel boundary
+//     publishes, plain loads read.
+// Every spin is bounded: a timeout sets d.tmo (pinned host memory) and every
+// workgroup drains.
 #pragma once
 #ifndef __HIPCC_RTC__   // (hiprtc, user families: the runtime provides these)
 #include <hip/hip_runtime.h>
@@ -109,6 +107,10 @@ struct Dev {
   unsigned* tmo;         // timeout word: pinned host memory, mapped (host reads it directly)
   // variates of iterations [vbase, vbase + vcap): filled by nmc_k_fill
   double* vzl;           // [t][P][G][C][2] {proposal normal, log accept uniform}
+  // zin: nmc_k_run draws each step's {z, log u} itself (nmc_step_variate, a job in the
+  // step's tile queue) and nmc_k_fill writes only the hyper variates; 0: the fill writes
+  // vzl and the control wave copies it into LDS (nmc_k_step, or NMC_ZIN=0)
+  int zin;
   double* vh;            // [t][P][C][2]    {hyper mean normal, hyper Gamma(a) draw}
   int vbase, vcap;
   const double* rz;      // replay [iter][P][G][C]
@@ -226,6 +228,24 @@ __device__ __forceinline__ int nmc_record_row(const Dev& d, int iter) {
   return row < d.n_rows ? row : -1;
 }
 
+// {z, log u} of step (it, p) of group g, chain c (the chain's global id is chain_base +
+// c): Philox4x32-10 normal and log of a 53-bit uniform, or the replayed reference
+// variates.  nmc_k_fill and nmc_k_run's variate job both call this, so a step's variates
+// never depend on which kernel drew them.
+enum { NMC_RNG_MODE_REPLAY = 1 };   // (include/nestmc.h NMC_RNG_REPLAY)
+__device__ __forceinline__ void nmc_step_variate(const Dev& d, int it, int p, int g, int c,
+                                                 double& z, double& lu) {
+  if (d.rng_mode == NMC_RNG_MODE_REPLAY) {
+    const size_t k = (((size_t)it * d.P + p) * d.G + g) * d.C + c;
+    z = it < d.replay_n ? d.rz[k] : nmc_nan();
+    lu = it < d.replay_n ? log(d.ru[k]) : nmc_nan();
+  } else {
+    const uint32_t ch = (uint32_t)(d.chain_base + c);
+    z = nmc_normal(it, g, p, NMC_PURPOSE_PROPOSAL, ch, d.seed);
+    lu = log(nmc_uniform2(it, g, p, NMC_PURPOSE_ACCEPT, ch, d.seed).a);
+  }
+}
+
 // Parameter.tune (posteriorSampling.py:385-437)
 __device__ __forceinline__ void nmc_tune(double& s, double& na, double& nr) {
   const double tot = na + nr;
@@ -332,13 +352,16 @@ __device__ __forceinline__ void nmc_drain_vm() { asm volatile("s_waitcnt vmcnt(0
 #endif
 template <int SRC, bool SQ>
 __device__ __forceinline__ void nmc_hyper_streams(const Dev& d, const double* src, int cc,
-                                                  double* lds, const nmc_lds_layout& L) {
+                                                  double* lds, const nmc_lds_layout& L,
+                                                  int ponly = -1) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int W = blockDim.x >> 6;
   const int P = d.P, G = d.G, C = d.C, nl = d.nleaf, ncol = 8 + d.ntail;
   const int per = 8 + (d.ntail ? 1 : 0);
-  const int nst = P * nl * per;
+  // the streams of every parameter, or of parameter ponly only
+  const int sbeg = ponly < 0 ? 0 : ponly * nl * per;
+  const int nst = ponly < 0 ? P * nl * per : (ponly + 1) * nl * per;
   // NS streams per wave-iteration, their loads in flight together
   constexpr int NS = NMC_HYPER_NS;
   struct Strm {
@@ -360,7 +383,7 @@ __device__ __forceinline__ void nmc_hyper_streams(const Dev& d, const double* sr
     return q;
   };
   const size_t xs = SRC == NMC_SRC_LDS ? 64 : (size_t)C;
-  for (int s0 = w; s0 < nst; s0 += W * NS) {
+  for (int s0 = sbeg + w; s0 < nst; s0 += W * NS) {
     double t[NS][16];
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
@@ -449,9 +472,12 @@ __device__ __forceinline__ void nmc_hyper_variates(const Dev& d, int cb, int t, 
               lds + L.hv * 64 + p * 128);
 }
 
+// ponly >= 0: the update of that parameter alone (the persistent all-wave mode updates
+// parameter p at step (t + 1, p), one step after the last publication it needs)
 template <int SRC>
 __device__ __forceinline__ void nmc_hyper(const Dev& d, const double* src, int cb, int t,
-                                          double* lds, const nmc_lds_layout& L, bool write) {
+                                          double* lds, const nmc_lds_layout& L, bool write,
+                                          int ponly = -1) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int W = blockDim.x >> 6;
@@ -459,19 +485,20 @@ __device__ __forceinline__ void nmc_hyper(const Dev& d, const double* src, int c
   const int c = nmc_lane_chain(d, cb, lane);
   const int cc = c < C ? c : C - 1;
   const bool own = nmc_lane_owns(d, c, lane);
-  nmc_hyper_streams<SRC, false>(d, src, cc, lds, L);
+  const int pb = ponly < 0 ? 0 : ponly, pe = ponly < 0 ? P : ponly + 1;
+  nmc_hyper_streams<SRC, false>(d, src, cc, lds, L, ponly);
   __syncthreads();
-  for (int p = w; p < P; p += W) {
+  for (int p = pb + w; p < pe; p += W) {
     const double tot = nmc_hyper_combine(d, lds, L, p, lane);
     const double sdm = lds[(L.hyp + NMC_HY_SDM * P + p) * 64 + lane];
     const double hz = lds[L.hv * 64 + (p * 64 + lane) * 2];
     lds[(L.hyp + NMC_HY_MU * P + p) * 64 + lane] = tot / G + sdm * hz;   // mu ~ N(mean(x), sqrt(s2/G))
   }
   __syncthreads();
-  nmc_hyper_streams<SRC, true>(d, src, cc, lds, L);
+  nmc_hyper_streams<SRC, true>(d, src, cc, lds, L, ponly);
   __syncthreads();
   const int row = write ? nmc_record_row(d, t) : -1;
-  for (int p = w; p < P; p += W) {
+  for (int p = pb + w; p < pe; p += W) {
     const double ss = nmc_hyper_combine(d, lds, L, p, lane);
     const double hat = ss / (double)(G - 1);
     const double scale = d.ha * hat;
@@ -1571,9 +1598,19 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   auto put_zl = [&](int tn, int pn, int slot) {
     nmc_dma16(zl_src(tn, pn), lds + (L.zl + 2 * slot) * 64);
   };
+  // ... or drawn here (d.zin): the calling wave's 64 lanes, one chain each
+  auto gen_zl = [&](int tn, int pn, int slot) {
+    double z, lu;
+    nmc_step_variate(d, tn, pn, g, cc, z, lu);
+    lds[(L.zl + 2 * slot) * 64 + 2 * lane] = z;
+    lds[(L.zl + 2 * slot) * 64 + 2 * lane + 1] = lu;
+  };
   double* cwv = lds + L.cw * 64 + lane;    // cwv[k * 64]: control-wave values across barriers
   if (ctl) {     // {z, log u} of the first step -> LDS slot of step i0*P
-    put_zl(i0, 0, (i0 * P) & 1);
+    if (d.zin)
+      gen_zl(i0, 0, (i0 * P) & 1);
+    else
+      put_zl(i0, 0, (i0 * P) & 1);
     for (int j = 0; j < Fam::NACC; ++j)   // x + (-0.0) == x: the fixed slot sum
       for (int k = nt; k < NMC_NSLOT; ++k) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = -0.0;
     nmc_drain_vm();
@@ -1650,10 +1687,18 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         k = __hip_atomic_fetch_add(tcnt + sp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       return k;
     };
-    int k = (int)__builtin_amdgcn_readlane(grab(), 0);
-    (void)t;
-    while (k < nt) {
+    // d.zin: queue entry 0 is the next step's variate job, entries 1.. the tiles
+    const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
+    const int zj = d.zin && tn < i1 ? 1 : 0;
+    int kq = (int)__builtin_amdgcn_readlane(grab(), 0);
+    while (kq < nt + zj) {
       const unsigned kn = grab();
+      if (kq < zj) {   // the variate job: {z, log u} of the next step -> the other slot
+        gen_zl(tn, pn, sp ^ 1);
+        kq = (int)__builtin_amdgcn_readlane(kn, 0);
+        continue;
+      }
+      const int k = kq - zj;
       const int ra = TI.start(k);
       const int rn = TI.len(k);
       NMC_TILE_STAMP(k, 0);
@@ -1681,7 +1726,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = acc[j];
       NMC_TILE_STAMP(k, 1);
       between();
-      k = (int)__builtin_amdgcn_readlane(kn, 0);
+      kq = (int)__builtin_amdgcn_readlane(kn, 0);
     }
   };
   // ---- register mode: the Gibbs wave runs its own loop, so its 64-value payload never
@@ -1815,9 +1860,11 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     for (int p = 0; p < P; ++p) {
       const int sp = (t * P + p) & 1;
       double c_prop, c_v, c_lu, c_lpc, c_lpp, c_sA, c_sR;   // control wave, this step
-      // Gibbs update of every parameter at step 0 (launch-per-iteration / fallback)
+      // Gibbs update of parameter p after iteration t-1 at step (t, p), right before the
+      // decision that needs it (all-wave modes: persistent SYNC, launch per iteration):
+      // the publications it waits for are a whole step old
       const bool hyper_now =
-          !hl && PARTIAL && p == 0 && t > 0 && !(t == i0 && (flags & NMC_RUN_HYPER_LOAD));
+          !hl && PARTIAL && t > 0 && !(t == i0 && (flags & NMC_RUN_HYPER_LOAD));
       // persistent Gibbs wave: the Gibbs update of parameter q after iteration tq is
       // task k = tq*P + q; every workgroup publishes it right after its decision at
       // global step k, so it is counted at the start of step k+1.  P == 1: the Gibbs
@@ -1957,7 +2004,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         }
         const int tn = p + 1 < P ? t : t + 1;
         const int pn = p + 1 < P ? p + 1 : 0;
-        if (tn < i1) put_zl(tn, pn, sp ^ 1);
+        if (tn < i1 && !d.zin) put_zl(tn, pn, sp ^ 1);   // (zin: the step's variate job)
             };
       bool ctl_done = !ctl;
       if (ctl) {
@@ -1987,12 +2034,12 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       double verdict = 0.0;
       if constexpr (hl) if (aux_now) verdict = lds[L.flag * 64 + 1];
       if constexpr (PARTIAL && !hl) if (hyper_now) {
-        if constexpr (sync) {   // every parameter of t-1 is published once P-1's count is full
-          ok = nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(t - i0), lds, L);
+        if constexpr (sync) {   // parameter p of t-1 is published once its count is full
+          ok = nmc_wait_published(d, cb, p, (unsigned)G * (unsigned)(t - i0), lds, L);
           if (!ok) break;
-          nmc_hyper<NMC_SRC_SC1>(d, ((t - 1) & 1) ? d.vb1 : d.vb0, cb, t - 1, lds, L, g0w);
+          nmc_hyper<NMC_SRC_SC1>(d, ((t - 1) & 1) ? d.vb1 : d.vb0, cb, t - 1, lds, L, g0w, p);
         } else {
-          nmc_hyper<NMC_SRC_GLOBAL>(d, ((t - 1) & 1) ? d.vb1 : d.vb0, cb, t - 1, lds, L, g0w);
+          nmc_hyper<NMC_SRC_GLOBAL>(d, ((t - 1) & 1) ? d.vb1 : d.vb0, cb, t - 1, lds, L, g0w, p);
         }
         if (ctl) {
           const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];

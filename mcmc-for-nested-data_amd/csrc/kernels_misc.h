@@ -12,7 +12,7 @@
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) nmc_k_fill(Dev d, int iter0, int T) {
   const size_t PGC = (size_t)d.P * d.G * d.C, PC = (size_t)d.P * d.C;
-  const size_t n1 = (size_t)T * PGC;
+  const size_t n1 = d.zin ? 0 : (size_t)T * PGC;   // (zin: the step kernel draws these)
   const size_t n2 = d.pooling == NMC_POOL_PARTIAL ? (size_t)T * PC : 0;
   for (size_t i0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i0 < n1 + n2;
        i0 += (size_t)gridDim.x * blockDim.x) {
@@ -26,15 +26,7 @@ __global__ void __launch_bounds__(256) nmc_k_fill(Dev d, int iter0, int T) {
       const int p = (int)(r / ((size_t)d.C * d.G));
       const int it = iter0 + t;
       double z, lu;
-      if (d.rng_mode == NMC_RNG_REPLAY) {
-        const size_t k = (size_t)it * PGC + r;
-        z = it < d.replay_n ? d.rz[k] : nmc_nan();
-        lu = it < d.replay_n ? log(d.ru[k]) : nmc_nan();
-      } else {
-        const uint32_t ch = (uint32_t)(d.chain_base + c);
-        z = nmc_normal(it, g, p, NMC_PURPOSE_PROPOSAL, ch, d.seed);
-        lu = log(nmc_uniform2(it, g, p, NMC_PURPOSE_ACCEPT, ch, d.seed).a);
-      }
+      nmc_step_variate(d, it, p, g, c, z, lu);
       d.vzl[2 * i] = z;
       d.vzl[2 * i + 1] = lu;
     } else {

@@ -414,6 +414,10 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     if (rc) { nmc_destroy(x); return rc; }
     HIPCHK(hipMemset(d.xcnt, 0, (size_t)d.RB * d.G * 32 * sizeof(unsigned)));
   }
+  // the step kernel draws its {z, log u} itself (a job in each step's tile queue) unless
+  // the opt-in one-barrier kernel runs (it DMAs them from the fill's ring); NMC_ZIN=0
+  // keeps the fill for every variate (bit-identical; tests compare them)
+  d.zin = !uses_step(x, run_mode(x)) && !(getenv("NMC_ZIN") && !atoi(getenv("NMC_ZIN")));
   d.thin = 1; d.tune_interval = 100;
   HIPCHK(hipMemcpy(off, group_offsets, (n_groups + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
   if (n_obs > 0)
@@ -613,7 +617,7 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       // every variate of iterations [c0, c1) in one fully parallel launch
       x->d.vbase = c0;
       const size_t n =
-          (size_t)(c1 - c0) * P * x->C * (x->G + (partial ? 1 : 0));
+          (size_t)(c1 - c0) * P * x->C * ((x->d.zin ? 0 : x->G) + (partial ? 1 : 0));
       if (n) {
         const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);
         hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);

@@ -204,6 +204,8 @@ def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
             # none pooling on few workgroups runs the half layout (32 chains per workgroup,
             # lane pairs on the two row parities); this keeps 64 chains per workgroup
             "full": {"NMC_HALF": "0"},
+            # step variates from the fill kernel's ring, not the step kernel's variate job
+            "fill": {"NMC_ZIN": "0"},
             # the opt-in one-barrier step kernel (step.h), both variant flags
             "step": {"NMC_STEP": "1", "NMC_STEP_FLAGS": "3"}}
     for name, env in envs.items():
@@ -216,4 +218,5 @@ def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
         assert numpy.array_equal(runs["paired"][k], runs["bcast"][k], equal_nan=True), k
         assert numpy.array_equal(runs["paired"][k], runs["step"][k], equal_nan=True), k
         assert numpy.array_equal(runs["paired"][k], runs["full"][k], equal_nan=True), k
+        assert numpy.array_equal(runs["paired"][k], runs["fill"][k], equal_nan=True), k
     assert runs["paired"][0].mean() > 0.02
