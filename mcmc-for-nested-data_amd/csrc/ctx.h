@@ -76,7 +76,7 @@ static inline size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
 static inline int run_mode(const nmc_ctx* x) {
   if (x->pooling != NMC_POOL_PARTIAL) return x->d.CL == 32 ? NMC_MODE_HALF : NMC_MODE_NOPOOL;
   if (!x->persistent) return NMC_MODE_LAUNCH;
-  if (x->d.hreg) return NMC_MODE_SYNC_REG;
+  if (x->d.hreg) return x->d.hown ? NMC_MODE_SYNC_OWN : NMC_MODE_SYNC_REG;
   return x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
 }
 
@@ -109,7 +109,8 @@ static inline int nmc_safe_blocks(const nmc_ctx* x, int nb) {
 }
 // mode of the persistent partial-pooling kernel (its occupancy query)
 static inline int nmc_persist_mode(const nmc_ctx* x) {
-  return x->d.hreg ? NMC_MODE_SYNC_REG : x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
+  return x->d.hreg ? (x->d.hown ? NMC_MODE_SYNC_OWN : NMC_MODE_SYNC_REG)
+                   : x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
 }
 // LDS of the persistent partial-pooling kernel (its occupancy query)
 static inline size_t nmc_persist_lds(const nmc_ctx* x) {

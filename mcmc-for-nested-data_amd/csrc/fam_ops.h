@@ -13,6 +13,7 @@ static const void* nmc_run_kernel_rl(int mode) {
     case NMC_MODE_LAUNCH: return (const void*)nmc_k_run<Fam, NMC_MODE_LAUNCH, RL>;
     case NMC_MODE_SYNC: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC, RL>;
     case NMC_MODE_SYNC_REG: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_REG, RL>;
+    case NMC_MODE_SYNC_OWN: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_OWN, RL>;
     case NMC_MODE_HALF:   // (rows in LDS, row pairs in every block: the host's condition)
       if constexpr (RL && nmc_paired_rows_ok<Fam>())
         return (const void*)nmc_k_run<Fam, NMC_MODE_HALF, true>;

@@ -107,9 +107,10 @@ struct Dev {
   unsigned* tmo;         // timeout word: pinned host memory, mapped (host reads it directly)
   // variates of iterations [vbase, vbase + vcap): filled by nmc_k_fill
   double* vzl;           // [t][P][G][C][2] {proposal normal, log accept uniform}
-  // zin: nmc_k_run draws each step's {z, log u} itself (nmc_step_variate, a job in the
-  // step's tile queue) and nmc_k_fill writes only the hyper variates; 0: the fill writes
-  // vzl and the control wave copies it into LDS (nmc_k_step, or NMC_ZIN=0)
+  // zin (build option NMC_ZIN_BUILD=1, measured slower): nmc_k_run draws each step's
+  // {z, log u} itself (nmc_step_variate, a job in the step's tile queue) and nmc_k_fill
+  // writes only the hyper variates; 0: the fill writes vzl and the control wave copies it
+  // into LDS
   int zin;
   double* vh;            // [t][P][C][2]    {hyper mean normal, hyper Gamma(a) draw}
   int vbase, vcap;
@@ -204,6 +205,11 @@ __device__ __forceinline__ nmc_pair2 nmc_halves(double v) {
 }
 
 enum { NMC_RUN_HYPER_LOAD = 1 };
+// Largest step-kernel workgroup (build option): 512 threads = 8 waves, 256 VGPRs per lane;
+// 768 = 12 waves (three per SIMD) caps the kernel at 168 VGPRs.
+#ifndef NMC_RUN_THREADS
+#define NMC_RUN_THREADS 512
+#endif
 // Likelihood tiles per group (nmc_tiles) = partial-sum slots per accumulator.
 #ifndef NMC_NSLOT_N
 #define NMC_NSLOT_N 16
@@ -233,6 +239,9 @@ __device__ __forceinline__ int nmc_record_row(const Dev& d, int iter) {
 // variates.  nmc_k_fill and nmc_k_run's variate job both call this, so a step's variates
 // never depend on which kernel drew them.
 enum { NMC_RNG_MODE_REPLAY = 1 };   // (include/nestmc.h NMC_RNG_REPLAY)
+#ifndef NMC_ZIN_BUILD
+#define NMC_ZIN_BUILD 0
+#endif
 __device__ __forceinline__ void nmc_step_variate(const Dev& d, int it, int p, int g, int c,
                                                  double& z, double& lu) {
   if (d.rng_mode == NMC_RNG_MODE_REPLAY) {
@@ -1438,12 +1447,15 @@ __device__ __forceinline__ void nmc_hyper_read(const Dev& d, int tq, int q, int 
   hy[(NMC_HY_ISD * P + q) * 64] = 1.0 / sd;
 }
 
+// STREAM = false (the register mode's instance) compiles only the G <= 64 path: the
+// streamed passes' code cost the cfg-3 kernel 740 more SGPR spills (903 against 166).
 // The register Gibbs update of task (tq, q) for this wave's 64 chains: G <= 64 from one
 // 64-value fetch (nmc_hyper_fetch_reg / _compute_reg), 64 < G <= 256 streamed
 // (nmc_pairwise_stream, two passes).  Same sums, draws and outputs either way.
+template <bool STREAM>
 __device__ __forceinline__ void nmc_hyper_update_reg(const Dev& d, int cb, int tq, int q, int cc,
                                                      double* lds, int hyp, bool write) {
-  if (d.G <= 64) {
+  if (!STREAM || d.G <= 64) {
     double xv[64], fz, fx;
     nmc_hyper_fetch_reg(d, tq, q, cc, xv, fz, fx);
     nmc_hyper_compute_reg(d, cb, tq, q, lds, hyp, write, fz, fx, xv);
@@ -1490,14 +1502,14 @@ enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
        NMC_MODE_SYNC_LDS = 3,    // persistent, the Gibbs wave works on an LDS copy
        NMC_MODE_SYNC_REG = 4,    // persistent, G <= 64: the Gibbs wave fetches the task's
                                  // values straight into registers and updates in one step
-                                 // (G > 64: the owner hand-off, Dev.hown; 5 = its report)
+       NMC_MODE_SYNC_OWN = 5,    // persistent, G > 64, opt-in: the owner hand-off (Dev.hown)
        NMC_MODE_HALF = 6 };      // none/complete pooling, 32 chains per workgroup: lanes l
                                  // and l + 32 hold chain l, on the two row parities
 // RL: the groups' rows are staged in LDS for the launch (d.rows_lds) -- a template
 // parameter so each instance holds only its own row loop (the LDS-DMA staged loop's
 // registers raised the rows-in-LDS kernel's pressure: ~5 % of its time at cfg 3)
 template <class Fam, int MODE, bool RL = true>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(NMC_RUN_THREADS)
 nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int flags) {
   constexpr bool PARTIAL = MODE != NMC_MODE_NOPOOL && MODE != NMC_MODE_HALF;
   // half layout: the grid of 64-chain blocks would leave CUs idle (none/complete pooling,
@@ -1520,10 +1532,12 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const bool live = nmc_lane_owns(d, c, lane) && mb == 0 && (!HALF || lane < 32);
   const bool g0w = g == 0 && mb == 0;   // writes the chain block's hyper-parameters
   const int cc = c < C ? c : C - 1;
-  constexpr bool sync =
-      MODE == NMC_MODE_SYNC || MODE == NMC_MODE_SYNC_LDS || MODE == NMC_MODE_SYNC_REG;
-  // Gibbs-wave modes: payload in LDS (two-stage pipeline) or in registers (one stage)
-  constexpr bool hr = MODE == NMC_MODE_SYNC_REG;
+  constexpr bool sync = MODE == NMC_MODE_SYNC || MODE == NMC_MODE_SYNC_LDS ||
+                        MODE == NMC_MODE_SYNC_REG || MODE == NMC_MODE_SYNC_OWN;
+  // Gibbs-wave modes: payload in LDS (two-stage pipeline) or in registers (one stage; the
+  // owner hand-off is its own instance, so its code never costs the register mode)
+  constexpr bool own = MODE == NMC_MODE_SYNC_OWN;
+  constexpr bool hr = MODE == NMC_MODE_SYNC_REG || own;
   constexpr bool hl = MODE == NMC_MODE_SYNC_LDS || hr;
   // the Gibbs wave's task at global step gs is gs - lag; the register mode updates a
   // task two steps after its publication (P >= 2: the hand-off latency -- store drain,
@@ -1533,7 +1547,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   // register mode: the task this workgroup closes after the loop (-1: none)
   const int close_k = [&]() {
     const int ge = i1 * P, k0 = ge - lag > i0 * P ? ge - lag : i0 * P;
-    return hr && mb == 0 && k0 + g < ge ? k0 + g : -1;
+    return hr && !own && mb == 0 && k0 + g < ge ? k0 + g : -1;
   }();
   // rows in LDS for the launch, or every wave's two staging buffers (nmc_ll_rows_staged)
   const int row_doubles = RL ? d.nmax * Fam::NFIELDS
@@ -1598,16 +1612,24 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   auto put_zl = [&](int tn, int pn, int slot) {
     nmc_dma16(zl_src(tn, pn), lds + (L.zl + 2 * slot) * 64);
   };
-  // ... or drawn here (d.zin): the calling wave's 64 lanes, one chain each
+  // ... or drawn here (d.zin, build option NMC_ZIN_BUILD=1): the calling wave's 64 lanes,
+  // one chain each.  Measured slower: with the Philox / Box-Muller / log code inlined
+  // into the tile loop the cfg-3 kernel spills twice the SGPRs (955 against 548) and runs
+  // 11.7 against 7.5 us/iter (profiles/r03d_*), more than the fill it saves (0.53 us/iter
+  // + 7 us per launch) -- so the shipped build keeps the fill.
   auto gen_zl = [&](int tn, int pn, int slot) {
+#if NMC_ZIN_BUILD
     double z, lu;
     nmc_step_variate(d, tn, pn, g, cc, z, lu);
     lds[(L.zl + 2 * slot) * 64 + 2 * lane] = z;
     lds[(L.zl + 2 * slot) * 64 + 2 * lane + 1] = lu;
+#else
+    (void)tn; (void)pn; (void)slot;
+#endif
   };
   double* cwv = lds + L.cw * 64 + lane;    // cwv[k * 64]: control-wave values across barriers
   if (ctl) {     // {z, log u} of the first step -> LDS slot of step i0*P
-    if (d.zin)
+    if (NMC_ZIN_BUILD && d.zin)
       gen_zl(i0, 0, (i0 * P) & 1);
     else
       put_zl(i0, 0, (i0 * P) & 1);
@@ -1689,7 +1711,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     };
     // d.zin: queue entry 0 is the next step's variate job, entries 1.. the tiles
     const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
-    const int zj = d.zin && tn < i1 ? 1 : 0;
+    const int zj = NMC_ZIN_BUILD && d.zin && tn < i1 ? 1 : 0;
     int kq = (int)__builtin_amdgcn_readlane(grab(), 0);
     while (kq < nt + zj) {
       const unsigned kn = grab();
@@ -1732,7 +1754,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   // ---- register mode: the Gibbs wave runs its own loop, so its 64-value payload never
   //      shares registers with the control code; after its update it takes likelihood
   //      tiles like every other wave, and it meets them at the same two barriers ----
-  if constexpr (hr) if (gw && d.hown) {
+  if constexpr (own) if (gw) {
     // owner hand-off (G > 64): at step gs the wave (a) reads task gs - lag, computed by its
     // owner, for this step's priors and (b) computes task gs - 1 when this workgroup owns
     // it (needed at step gs - 1 + P); P == 1 needs task gs - 1 at once: (b) before (a)
@@ -1744,7 +1766,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       if (!nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1))) return false;
       // keep the payload loads below the poll (no instruction: wavefront scope)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      nmc_hyper_update_reg(d, cb, kt, kq, cc, lds, L.hyp, true);
+      nmc_hyper_update_reg<true>(d, cb, kt, kq, cc, lds, L.hyp, true);
       nmc_drain_vm();   // the hyper-parameters are stored before they are counted
       if (lane == 0)
         __hip_atomic_fetch_add(nmc_hrd(d, cb, kq), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1793,7 +1815,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     // other waves' nmc_wait_published); every earlier task was computed in the loop
     if (ok && own && nmc_task_owner(d, i1 * P - 1) == g) {
       if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L)) {
-        nmc_hyper_update_reg(d, cb, i1 - 1, P - 1, cc, lds, L.hyp, true);
+        nmc_hyper_update_reg<true>(d, cb, i1 - 1, P - 1, cc, lds, L.hyp, true);
         nmc_drain_vm();
         if (lane == 0)
           __hip_atomic_fetch_add(nmc_hrd(d, cb, P - 1), 1u, __ATOMIC_RELAXED,
@@ -1803,7 +1825,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     nmc_drain_vm();
     return;
   }
-  if constexpr (hr) if (gw) {
+  if constexpr (hr && !own) if (gw) {
     const int gs0 = i0 * P;
     for (int t = i0; t < i1 && ok; ++t) {
       for (int p = 0; p < P; ++p) {
@@ -1819,7 +1841,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
           if (r) {
             // keep the payload loads below the poll (no instruction: wavefront scope)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            nmc_hyper_update_reg(d, cb, kt, kq, cc, lds, L.hyp, g0w);
+            nmc_hyper_update_reg<false>(d, cb, kt, kq, cc, lds, L.hyp, g0w);
             if (p == 0) NMC_STAMP_AUX(t, 15);
             if (P <= 2) {   // the update lands in the step that needs it: this step's priors
               const int sp = gs & 1;
@@ -1848,7 +1870,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     if (ok && close_k >= 0) {
       if (nmc_wait_published(d, cb, close_k % P, (unsigned)G * (unsigned)(close_k / P - i0 + 1),
                              lds, L))
-        nmc_hyper_update_reg(d, cb, close_k / P, close_k % P, cc, lds, L.hyp, true);
+        nmc_hyper_update_reg<false>(d, cb, close_k / P, close_k % P, cc, lds, L.hyp, true);
     }
     nmc_drain_vm();
     return;
@@ -2004,7 +2026,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         }
         const int tn = p + 1 < P ? t : t + 1;
         const int pn = p + 1 < P ? p + 1 : 0;
-        if (tn < i1 && !d.zin) put_zl(tn, pn, sp ^ 1);   // (zin: the step's variate job)
+        if (tn < i1 && !(NMC_ZIN_BUILD && d.zin)) put_zl(tn, pn, sp ^ 1);   // (zin: the job)
             };
       bool ctl_done = !ctl;
       if (ctl) {
@@ -2135,9 +2157,8 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   }
   // ---- closing Gibbs updates after i1-1 (group-0 workgroups write and record them; the
   //      owner hand-off: the last task's owner) ----
-  if constexpr (hl) if (ok && (hr ? (d.hown ? mb == 0 && nmc_task_owner(d, i1 * P - 1) == g
-                                           : close_k >= 0)
-                                  : g0w)) {
+  if constexpr (hl) if (ok && (own ? mb == 0 && nmc_task_owner(d, i1 * P - 1) == g
+                                  : hr ? close_k >= 0 : g0w)) {
     const int ge = i1 * P;   // tasks ge-2 (copied at the last step; P >= 2) and ge-1 are left
     if (!hr && P >= 2 && gw) {
       const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 2)) * C + cc) * 2;
@@ -2145,7 +2166,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
                         ((ge - 2) & 1) * (G + 1));
     }
     // (register mode: the Gibbs wave closes in its own loop; this is the matching barrier)
-    const int wk = hr && !d.hown ? close_k : ge - 1;   // the task whose publication is awaited
+    const int wk = hr && !own ? close_k : ge - 1;   // the task whose publication is awaited
     const bool pub = nmc_wait_published(d, cb, wk % P, (unsigned)G * (unsigned)(wk / P - i0 + 1),
                                         lds, L);
     if (!hr && pub && gw) {

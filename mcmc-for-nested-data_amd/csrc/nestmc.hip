@@ -60,12 +60,12 @@ static void choose_geometry(nmc_ctx* x) {
   Dev& d = x->d;
   int64_t w = 1 + (d.nmax + 63) / 64;
   if (x->pooling == NMC_POOL_PARTIAL && w >= 2) w += 1;
-  if (w > 8) w = 8;
+  if (w > 8) w = 8;   // (a 768-thread build runs 12 only when asked: NMC_WAVES)
   if (w < 1) w = 1;
   d.CL = 64;   // one chain per lane, every kernel
   if (const char* e = getenv("NMC_WAVES")) {
     const int v = atoi(e);
-    if (v >= 1 && v <= 8) w = v;
+    if (v >= 1 && v <= NMC_RUN_THREADS / 64) w = v;
   }
   d.RB = (d.C + d.CL - 1) / d.CL;
   d.W = (int)w;
@@ -414,10 +414,11 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     if (rc) { nmc_destroy(x); return rc; }
     HIPCHK(hipMemset(d.xcnt, 0, (size_t)d.RB * d.G * 32 * sizeof(unsigned)));
   }
-  // the step kernel draws its {z, log u} itself (a job in each step's tile queue) unless
-  // the opt-in one-barrier kernel runs (it DMAs them from the fill's ring); NMC_ZIN=0
-  // keeps the fill for every variate (bit-identical; tests compare them)
-  d.zin = !uses_step(x, run_mode(x)) && !(getenv("NMC_ZIN") && !atoi(getenv("NMC_ZIN")));
+  // build option NMC_ZIN_BUILD=1: the step kernel draws its {z, log u} itself (a job in
+  // each step's tile queue) unless the opt-in one-barrier kernel runs (it DMAs them from
+  // the fill's ring); NMC_ZIN=0 keeps the fill (bit-identical; tests compare them)
+  d.zin = NMC_ZIN_BUILD && !uses_step(x, run_mode(x)) &&
+          !(getenv("NMC_ZIN") && !atoi(getenv("NMC_ZIN")));
   d.thin = 1; d.tune_interval = 100;
   HIPCHK(hipMemcpy(off, group_offsets, (n_groups + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
   if (n_obs > 0)
@@ -803,7 +804,7 @@ int nmc_split_config(nmc_ctx* x, int* members, int* chain_blocks_per_launch) {
 
 int nmc_kernel_name(nmc_ctx* x, char* out, int cap) {
   static const char* const modes[] = {"NMC_MODE_NOPOOL", "NMC_MODE_LAUNCH", "NMC_MODE_SYNC",
-                                      "NMC_MODE_SYNC_LDS", "NMC_MODE_SYNC_REG", "",
+                                      "NMC_MODE_SYNC_LDS", "NMC_MODE_SYNC_REG", "NMC_MODE_SYNC_OWN",
                                       "NMC_MODE_HALF"};
   const int mode = run_mode(x);
   std::string fam;
@@ -828,9 +829,7 @@ int nmc_launch_config(nmc_ctx* x, int* waves_per_group, int* chain_blocks, int* 
   *chain_blocks = x->d.RB;
   if (persistent) *persistent = x->persistent || x->pooling != NMC_POOL_PARTIAL ? 1 : 0;
   if (chains_per_block) *chains_per_block = x->d.CL;
-  // (5: the register mode with the owner hand-off, G > 64 -- reported only; the kernel
-  // instance is the SYNC_REG one)
-  if (mode) *mode = run_mode(x) == NMC_MODE_SYNC_REG && x->d.hown ? 5 : run_mode(x);
+  if (mode) *mode = run_mode(x);
   return 0;
 }
 

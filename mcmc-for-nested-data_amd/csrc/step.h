@@ -1,6 +1,8 @@
-// step.h -- the one-barrier step kernel: nmc_k_step<Fam, MODE>, the production path for
-// groups whose rows fit LDS (cfg 2/3 and every shard of the same shape), none/complete
-// pooling (NOPOOL) and partial pooling with the register Gibbs hand-off (SYNC_REG).
+// step.h -- the one-barrier step kernel: nmc_k_step<Fam, MODE>, an opt-in (NMC_STEP=1)
+// alternative to nmc_k_run for groups whose rows fit LDS, none/complete pooling (NOPOOL)
+// and partial pooling with the register Gibbs hand-off (SYNC_REG).  Measured slower on
+// MI355X (cfg 3: 8.8-11.7 against 8.0 us/iter, profiles/r03_step_kernel_ab.json), kept
+// bit-identical and tested.
 //
 // Same work, partition and summation orders as nmc_k_run (kernels.h) -- the two are
 // bit-identical and the tests compare them -- but with ONE workgroup barrier per

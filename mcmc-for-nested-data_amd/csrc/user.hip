@@ -23,16 +23,17 @@
 namespace {
 
 // kernel table entries, in name-expression order
-// (nmc_k_run: mode m with rows in LDS at UK_RUN0 + m, rows staged at UK_RUN0 + 5 + m;
-// nmc_k_step: NOPOOL / SYNC_REG at UK_STEP0 / UK_STEP0 + 1)
-enum { UK_RUN0 = 0, UK_NRUN = 5, UK_GROUP_LL = 10, UK_OBS_LL_ROWS = 11, UK_OBS_LL = 12,
-       UK_STEP0 = 13, UK_GROUP_LL_RL = 15, UK_GROUP_FIN = 16, UK_HALF = 17, UK_N = 18 };
+// (nmc_k_run: mode m (0..5) with rows in LDS at UK_RUN0 + m, rows staged at UK_RUN0 + 6 + m;
+// nmc_k_step: NOPOOL / SYNC_REG at UK_STEP0 / UK_STEP0 + 1; the half layout at UK_HALF)
+enum { UK_RUN0 = 0, UK_NRUN = 6, UK_GROUP_LL = 12, UK_OBS_LL_ROWS = 13, UK_OBS_LL = 14,
+       UK_STEP0 = 15, UK_GROUP_LL_RL = 17, UK_GROUP_FIN = 18, UK_HALF = 19, UK_N = 20 };
 const char* const kNames[UK_N] = {
     "nmc_k_run<FamUser, 0, true>", "nmc_k_run<FamUser, 1, true>", "nmc_k_run<FamUser, 2, true>",
-    "nmc_k_run<FamUser, 3, true>", "nmc_k_run<FamUser, 4, true>",
+    "nmc_k_run<FamUser, 3, true>", "nmc_k_run<FamUser, 4, true>", "nmc_k_run<FamUser, 5, true>",
     "nmc_k_run<FamUser, 0, false>", "nmc_k_run<FamUser, 1, false>",
     "nmc_k_run<FamUser, 2, false>", "nmc_k_run<FamUser, 3, false>",
-    "nmc_k_run<FamUser, 4, false>", "nmc_k_group_part<FamUser, false>", "nmc_k_obs_ll_rows<FamUser>",
+    "nmc_k_run<FamUser, 4, false>", "nmc_k_run<FamUser, 5, false>",
+    "nmc_k_group_part<FamUser, false>", "nmc_k_obs_ll_rows<FamUser>",
     "nmc_k_obs_ll<FamUser>", "nmc_k_step<FamUser, 0>", "nmc_k_step<FamUser, 4>",
     "nmc_k_group_part<FamUser, true>", "nmc_k_group_fin<FamUser>",
     "nmc_k_run<FamUser, 6, true>"};
@@ -145,7 +146,10 @@ extern "C" int nmc_user_family_compile(const char* source, int n_fields, int n_p
   const std::string defs = "#define NMC_NSLOT_N " + std::to_string((int)NMC_NSLOT) +
                            "\n#define NMC_HYPER_NS " + std::to_string((int)NMC_HYPER_NS) +
                            "\n#define NMC_LDS_ROW_DOUBLES " +
-                           std::to_string((int)NMC_LDS_ROW_DOUBLES) + "\n"
+                           std::to_string((int)NMC_LDS_ROW_DOUBLES) +
+                           "\n#define NMC_RUN_THREADS " + std::to_string((int)NMC_RUN_THREADS) +
+                           "\n#define NMC_ZIN_BUILD " + std::to_string((int)NMC_ZIN_BUILD) +
+                           "\n"
 #ifdef NMC_STAMPS
                            "#define NMC_STAMPS 1\n"
 #endif
