@@ -5,50 +5,47 @@
 #include "kernels.h"
 
 // ---------------------------------------------------------------------------
-// Variates for iterations [iter0, iter0 + T): one thread per (t, p, g, c) element
-// of the step variates and per (t, p, c) of the hyper variates.  The hyper variates come
-// first in the index space: their Gamma draws (rejection loops) are the longest threads,
-// and started first they run under the bulk of the step variates instead of after it.
+// Variates for iterations [iter0, iter0 + T), two kernels so the short step-variate one
+// is not held to the Gamma draws' registers (one kernel: 153 VGPRs, 3 waves per SIMD):
+//   nmc_k_fill        one thread per (t, p, g, c): {z, log u} of the step (Philox normal,
+//                     log of a 53-bit uniform, or the replayed reference variates);
+//   nmc_k_fill_hyper  one thread per (t, p, c): {hyper z, Gamma((G-1)/2)} (Marsaglia-Tsang
+//                     on the Philox stream, or gammainccinv of the replayed uniform).
+// The variate ring holds at most 1 GiB, so every element index fits 32 bits.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) nmc_k_fill(Dev d, int iter0, int T) {
-  const size_t PGC = (size_t)d.P * d.G * d.C, PC = (size_t)d.P * d.C;
-  const size_t n1 = d.zin ? 0 : (size_t)T * PGC;   // (zin: the step kernel draws these)
-  const size_t n2 = d.pooling == NMC_POOL_PARTIAL ? (size_t)T * PC : 0;
-  for (size_t i0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i0 < n1 + n2;
-       i0 += (size_t)gridDim.x * blockDim.x) {
-    // i0 < n2: hyper element i0; else step element i0 - n2
-    const size_t i = i0 < n2 ? n1 + i0 : i0 - n2;
-    if (i < n1) {
-      const int t = (int)(i / PGC);
-      const size_t r = i % PGC;
-      const int c = (int)(r % d.C);
-      const int g = (int)((r / d.C) % d.G);
-      const int p = (int)(r / ((size_t)d.C * d.G));
-      const int it = iter0 + t;
-      double z, lu;
-      nmc_step_variate(d, it, p, g, c, z, lu);
-      d.vzl[2 * i] = z;
-      d.vzl[2 * i + 1] = lu;
+  const unsigned C = (unsigned)d.C, GC = (unsigned)d.G * C, PGC = (unsigned)d.P * GC;
+  const unsigned n1 = d.zin ? 0u : (unsigned)T * PGC;   // (zin: the step kernel draws these)
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n1; i += gridDim.x * blockDim.x) {
+    const unsigned t = i / PGC, r = i - t * PGC;
+    const unsigned p = r / GC, q = r - p * GC;
+    const unsigned g = q / C, c = q - g * C;
+    double z, lu;
+    nmc_step_variate(d, iter0 + (int)t, (int)p, (int)g, (int)c, z, lu);
+    d.vzl[2 * (size_t)i] = z;
+    d.vzl[2 * (size_t)i + 1] = lu;
+  }
+}
+
+__global__ void __launch_bounds__(256) nmc_k_fill_hyper(Dev d, int iter0, int T) {
+  const unsigned C = (unsigned)d.C, PC = (unsigned)d.P * C;
+  const unsigned n2 = (unsigned)T * PC;
+  for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < n2; j += gridDim.x * blockDim.x) {
+    const unsigned t = j / PC, r = j - t * PC;
+    const unsigned p = r / C, c = r - p * C;
+    const int it = iter0 + (int)t;
+    double hz, hx;
+    if (d.rng_mode == NMC_RNG_REPLAY) {
+      const size_t k = (size_t)it * PC + r;
+      hz = it < d.replay_n ? d.rhz[k] : nmc_nan();
+      hx = it < d.replay_n ? nmc_igamci(d.ha, d.rhu[k], d.hlga) : nmc_nan();
     } else {
-      const size_t j = i - n1;
-      const int t = (int)(j / PC);
-      const size_t r = j % PC;
-      const int c = (int)(r % d.C);
-      const int p = (int)(r / d.C);
-      const int it = iter0 + t;
-      double hz, hx;
-      if (d.rng_mode == NMC_RNG_REPLAY) {
-        const size_t k = (size_t)it * PC + r;
-        hz = it < d.replay_n ? d.rhz[k] : nmc_nan();
-        hx = it < d.replay_n ? nmc_igamci(d.ha, d.rhu[k], d.hlga) : nmc_nan();
-      } else {
-        const uint32_t ch = (uint32_t)(d.chain_base + c);
-        hz = nmc_normal(it, 0, p, NMC_PURPOSE_HYPER_NORMAL, ch, d.seed);
-        hx = nmc_gamma_mt(d.ha, it, p, ch, d.seed);
-      }
-      d.vh[2 * j] = hz;
-      d.vh[2 * j + 1] = hx;
+      const uint32_t ch = (uint32_t)(d.chain_base + (int)c);
+      hz = nmc_normal(it, 0, p, NMC_PURPOSE_HYPER_NORMAL, ch, d.seed);
+      hx = nmc_gamma_mt(d.ha, it, p, ch, d.seed);
     }
+    d.vh[2 * (size_t)j] = hz;
+    d.vh[2 * (size_t)j + 1] = hx;
   }
 }
 

@@ -615,13 +615,20 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
         x->launch_iters > 0 && x->launch_iters < x->d.vcap ? x->launch_iters : x->d.vcap;
     for (int c0 = iter_begin; c0 < iter_end; c0 += chunk) {
       const int c1 = c0 + chunk < iter_end ? c0 + chunk : iter_end;
-      // every variate of iterations [c0, c1) in one fully parallel launch
+      // every variate of iterations [c0, c1): the hyper variates (partial pooling), then
+      // the step variates (unless the step kernel draws them), each one parallel launch
       x->d.vbase = c0;
-      const size_t n =
-          (size_t)(c1 - c0) * P * x->C * ((x->d.zin ? 0 : x->G) + (partial ? 1 : 0));
-      if (n) {
-        const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);
-        hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);
+      auto blocks_for = [](size_t n) { return (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384); };
+      const size_t nh = partial ? (size_t)(c1 - c0) * P * x->C : 0;
+      const size_t ns = x->d.zin ? 0 : (size_t)(c1 - c0) * P * x->C * x->G;
+      if (nh) {
+        hipLaunchKernelGGL(nmc_k_fill_hyper, dim3(blocks_for(nh)), dim3(256), 0, x->stream, x->d,
+                           c0, c1 - c0);
+        HIPCHK(hipGetLastError());
+      }
+      if (ns) {
+        hipLaunchKernelGGL(nmc_k_fill, dim3(blocks_for(ns)), dim3(256), 0, x->stream, x->d, c0,
+                           c1 - c0);
         HIPCHK(hipGetLastError());
       }
       // counters continue from the earlier launches (Dev.pbase / xbase): reset only
