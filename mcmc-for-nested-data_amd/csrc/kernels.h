@@ -1882,6 +1882,10 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     for (int p = 0; p < P; ++p) {
       const int sp = (t * P + p) & 1;
       double c_prop, c_v, c_lu, c_lpc, c_lpp, c_sA, c_sR;   // control wave, this step
+      // the proposal's prepared parameters, formed before barrier A (the other values
+      // cannot change before the decision), so only the slot sum, finish and the
+      // Metropolis test remain between the barriers
+      typename Fam::Reg c_reg{};
       // Gibbs update of parameter p after iteration t-1 at step (t, p), right before the
       // decision that needs it (all-wave modes: persistent SYNC, launch per iteration):
       // the publications it waits for are a whole step old
@@ -1987,6 +1991,13 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         c_prop = c_v + (1.0 * s) * lds[(L.zl + 2 * sp) * 64 + 2 * lane];   // propose (:304-306)
         c_lu = lds[(L.zl + 2 * sp) * 64 + 2 * lane + 1];
         {
+          double thp[Fam::MAXP];
+#pragma unroll
+          for (int q = 0; q < Fam::MAXP; ++q)
+            thp[q] = q < P ? (q == p ? c_prop : th[q * 64]) : 0.0;
+          c_reg = fam.prepare(thp);
+        }
+        {
           const double na = st[(NMC_ST_NA * P + p) * 64], nr = st[(NMC_ST_NR * P + p) * 64];
           double naA = na + 1.0, nrA = nr, naR = na, nrR = nr + 1.0;
           c_sA = s;
@@ -2084,11 +2095,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         if (S > 1)   // row split: every member's partials, in member order
           nmc_split_exchange(d, cb, g, mb, t * P + p - i0 * P, acc);
         if (p == 0) NMC_STAMP(t, 10);
-        double thp[Fam::MAXP];
-#pragma unroll
-        for (int q = 0; q < Fam::MAXP; ++q) thp[q] = q < P ? (q == p ? c_prop : th[q * 64]) : 0.0;
-        const typename Fam::Reg reg = fam.prepare(thp);
-        const double llp = fam.finish_fast(reg, acc, (long)ngrp, gcst);
+        const double llp = fam.finish_fast(c_reg, acc, (long)ngrp, gcst);
         if (p == 0) NMC_STAMP(t, 11);
         if (hl && post_prior) {   // the Gibbs wave evaluated this step's priors
           c_lpc = cwv[NMC_CW_LPC * 64];

@@ -251,7 +251,10 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) { delete x; return fail(-2, std::string("hipSetDevice: ") + hipGetErrorString(e)); }
   e = hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking);
-  if (e != hipSuccess) { delete x; return fail(-2, std::string("hipStreamCreate: ") + hipGetErrorString(e)); }
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&x->join, hipEventDisableTiming);
+  if (e != hipSuccess) { nmc_destroy(x); return fail(-2, std::string("hipStreamCreate: ") + hipGetErrorString(e)); }
   for (auto& ev : x->ev) hipEventCreate(&ev);
 
   Dev& d = x->d;
@@ -438,11 +441,15 @@ int nmc_destroy(nmc_ctx* x) {
   if (!x) return 0;
   hipSetDevice(x->device);
   if (x->stream) hipStreamSynchronize(x->stream);
+  if (x->side) hipStreamSynchronize(x->side);
   for (void* p : x->owned) if (p) hipFree(p);
   for (auto& ev : x->ev) if (ev) hipEventDestroy(ev);
   for (auto& pr : x->kev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   for (auto& pr : x->hev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   if (x->stream) hipStreamDestroy(x->stream);
+  if (x->side) hipStreamDestroy(x->side);
+  if (x->fork) hipEventDestroy(x->fork);
+  if (x->join) hipEventDestroy(x->join);
   if (x->tmo_host) hipHostFree((void*)x->tmo_host);
   delete x;
   return 0;
@@ -621,16 +628,23 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       auto blocks_for = [](size_t n) { return (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384); };
       const size_t nh = partial ? (size_t)(c1 - c0) * P * x->C : 0;
       const size_t ns = x->d.zin ? 0 : (size_t)(c1 - c0) * P * x->C * x->G;
+      // (the hyper fill -- a few latency-bound Gamma draws -- runs on the side stream,
+      // concurrently with the step-variate fill; it waits for everything queued before it,
+      // so it never overwrites variates a running step kernel still reads)
       if (nh) {
-        hipLaunchKernelGGL(nmc_k_fill_hyper, dim3(blocks_for(nh)), dim3(256), 0, x->stream, x->d,
+        HIPCHK(hipEventRecord(x->fork, x->stream));
+        HIPCHK(hipStreamWaitEvent(x->side, x->fork, 0));
+        hipLaunchKernelGGL(nmc_k_fill_hyper, dim3(blocks_for(nh)), dim3(256), 0, x->side, x->d,
                            c0, c1 - c0);
         HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(x->join, x->side));
       }
       if (ns) {
         hipLaunchKernelGGL(nmc_k_fill, dim3(blocks_for(ns)), dim3(256), 0, x->stream, x->d, c0,
                            c1 - c0);
         HIPCHK(hipGetLastError());
       }
+      if (nh) HIPCHK(hipStreamWaitEvent(x->stream, x->join, 0));
       // counters continue from the earlier launches (Dev.pbase / xbase): reset only
       // before they could wrap
       const uint64_t steps = (uint64_t)(c1 - c0) * P;

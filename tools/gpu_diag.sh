@@ -14,6 +14,7 @@ echo "== phase stamps $(date +%T)"
 timeout -k 10 120 python3 tools/stamps.py partial > gpurun_out/stamps_$TAG.json 2>&1 || exit $?
 timeout -k 10 120 python3 tools/tilegantt.py > gpurun_out/tilegantt_$TAG.json 2>&1 || exit $?
 cut -c1-1500 gpurun_out/stamps_$TAG.json
+[ "${PMC:-1}" = 0 ] && exit 0
 echo "== pmc $(date +%T)"
 bash tools/pmc_profiles.sh $TAG || exit $?
 for w in cfg3 cfg3long cfg4 cfg5; do

@@ -29,7 +29,7 @@ def main():
     eng.lib.nmc_debug_stamps(eng.h, 0, out)
     st = numpy.frombuffer(out, dtype=numpy.uint64).astype(numpy.float64)
     ph = st[:512].reshape(2, 2, 8, 16)
-    ts = st[512:].reshape(8, 16, 4)
+    ts = st[512:1024].reshape(8, 16, 4)
     res = []
     for s in range(2, 8):
         tiles = [(k, int(ts[s, k, 2]), ts[s, k, 0], ts[s, k, 1]) for k in range(16) if ts[s, k, 1] > 0]
