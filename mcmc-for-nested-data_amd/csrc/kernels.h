@@ -210,6 +210,9 @@ enum { NMC_RUN_HYPER_LOAD = 1 };
 #ifndef NMC_RUN_THREADS
 #define NMC_RUN_THREADS 512
 #endif
+#ifndef NMC_GIBBS_TILES
+#define NMC_GIBBS_TILES 0
+#endif
 // Likelihood tiles per group (nmc_tiles) = partial-sum slots per accumulator.
 #ifndef NMC_NSLOT_N
 #define NMC_NSLOT_N 16
@@ -1856,6 +1859,9 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
             }
           }
         }
+#if NMC_GIBBS_TILES   // (A/B build option: the Gibbs wave takes likelihood tiles after its task)
+        lik_tiles(t, p, gs & 1, [] {});
+#endif
         __syncthreads();   // A
         if (due) {
           ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);

@@ -87,3 +87,60 @@ def test_devices_replay_writes_reference_csvs(gpu_lib, tmp_path, name):
     for ch in range(c.n_chains):
         mine = os.path.join(out, "sample", "sample.%i.csv" % ch)
         assert filecmp.cmp(mine, c.csv_path(ch), shallow=False), (name, ch)
+
+
+# ---- two processes (gloo ranks), each driving its own engine on the GPU ----------------
+def _gloo_engine_worker(rank, world, port, q):
+    """Rank `rank`: its contiguous shard of the chains (nestmc.parallel.shard), run by an
+    engine with chain_base = the shard's first global id; the recorded rows travel to
+    rank 0 over gloo, and bench.py's max-over-ranks timing reduction runs too."""
+    import torch.distributed as dist
+    from nestmc import parallel
+    from gpu_cases import partial_state, run_engine, synthetic
+    try:
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port,
+                                world_size=world, rank=rank)
+        C, G, N, n_iter, seed = 70, 5, 30, 24, 19
+        fam, sizes, _, _, _ = synthetic("linreg_partial", C, G, N)
+        st, _ = partial_state(fam, sizes, C, 2)
+        start, count = parallel.shard(C, world, rank)
+        sel = numpy.arange(start, start + count)
+        acc, _, rows, _ = run_engine(fam, sizes, st, sel, start, n_iter, seed)
+        t = parallel.max_over_ranks(1.0 + rank, dist)
+        out = [None] * world
+        dist.all_gather_object(out, (start, count, acc, rows))
+        if rank == 0:
+            whole = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed)
+            q.put(("ok", t, out, whole[0], whole[2]))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:   # reported to the parent
+        q.put(("error", repr(e), None, None, None))
+
+
+def test_two_gloo_ranks_engines_reproduce_one_engine(gpu_lib):
+    """The N > 1 path with the engine on every rank: two processes, one gloo
+    group, each samples its chain shard on the device; the shards are the one-engine run
+    bit for bit (every variate keyed by global chain id)."""
+    import socket
+    import torch.multiprocessing as mp
+    world = 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_engine_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    status, t, shards, acc1, rows1 = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    assert status == "ok", t
+    assert t == float(world)
+    assert [sh[0] for sh in shards] == [0, 35] and [sh[1] for sh in shards] == [35, 35]
+    assert numpy.array_equal(numpy.concatenate([sh[2] for sh in shards], 0), acc1)
+    assert numpy.array_equal(numpy.concatenate([sh[3] for sh in shards], 0), rows1,
+                             equal_nan=True)

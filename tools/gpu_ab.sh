@@ -1,19 +1,18 @@
 #!/bin/bash
-# A/B of step-kernel builds on one box: each variant runs the driver's bench command and the
-# default-length bench (no PMC, no CPU leg).  usage: tools/gpu_ab.sh TAG "NAME:ENV ..."
+# A/B of the shipped library against a variant library at cfg 3 (bench.py 2000 iterations,
+# kernel us/iter from its HIP-event pass), alternating A B A B.
+#   usage: tools/gpu_ab.sh TAG VARIANT_LIB [ENV...]
 set -o pipefail
-TAG=$1; shift
+TAG=${1:-ab}; LIB=$2; shift 2
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
-for v in "$@"; do
-  name=${v%%:*}; envs=${v#*:}
-  echo "== $name ($envs) $(date +%T)"
-  env $envs timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-pmc --cpu-seconds 0 \
-      > gpurun_out/ab_${TAG}_${name}_20.json 2> gpurun_out/ab_${TAG}_${name}_20.err || exit $?
-  env $envs timeout -k 10 200 python3 bench.py --no-pmc --cpu-seconds 0 \
-      > gpurun_out/ab_${TAG}_${name}.json 2> gpurun_out/ab_${TAG}_${name}.err || exit $?
-  python3 -c "
-import json,sys
-a=json.load(open('gpurun_out/ab_${TAG}_${name}_20.json')); b=json.load(open('gpurun_out/ab_${TAG}_${name}.json'))
-print('$name', 'bench20 %.4g' % a['value'], 'bench2000 %.4g' % b['value'], 'kernel_us/iter %.3f' % (b['roofline']['avg_launch_us']/b['roofline']['iterations_per_launch']), b['config']['launch']['waves_per_group'], b['roofline']['kernel'])"
+run() {   # name, env...
+  local name=$1; shift
+  env "$@" timeout -k 10 200 python3 bench.py --no-pmc --cpu-seconds 0 \
+      > gpurun_out/ab_${TAG}_$name.json 2> gpurun_out/ab_${TAG}_$name.err || return $?
+  python3 -c "import json; d=json.load(open('gpurun_out/ab_${TAG}_$name.json')); r=d['roofline']; print('$name', '%.4g' % d['value'], 'kernel us/iter %.3f' % (r['avg_launch_us'] / r['iterations_per_launch']), d['config']['launch']['mode'], 'W', d['config']['launch']['waves_per_group'])"
+}
+for k in 1 2; do
+  run base$k || exit $?
+  run var$k NESTMC_LIB=$LIB "$@" || exit $?
 done
