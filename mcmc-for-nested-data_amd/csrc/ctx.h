@@ -30,8 +30,6 @@ int nmc_fail(int code, const std::string& msg);
 struct nmc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t side = nullptr;              // the hyper-variate fill, beside the step-variate fill
-  hipEvent_t fork = nullptr, join = nullptr;
   int C = 0, chain_base = 0, G = 0, P = 0, pooling = 0, family = 0, nf = 0, rng = 0;
   uint32_t seed = 0;
   int64_t n_obs = 0;

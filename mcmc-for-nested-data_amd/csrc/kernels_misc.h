@@ -5,47 +5,49 @@
 #include "kernels.h"
 
 // ---------------------------------------------------------------------------
-// Variates for iterations [iter0, iter0 + T), two kernels so the short step-variate one
-// is not held to the Gamma draws' registers (one kernel: 153 VGPRs, 3 waves per SIMD):
-//   nmc_k_fill        one thread per (t, p, g, c): {z, log u} of the step (Philox normal,
-//                     log of a 53-bit uniform, or the replayed reference variates);
-//   nmc_k_fill_hyper  one thread per (t, p, c): {hyper z, Gamma((G-1)/2)} (Marsaglia-Tsang
-//                     on the Philox stream, or gammainccinv of the replayed uniform).
-// The variate ring holds at most 1 GiB, so every element index fits 32 bits.
+// Variates for iterations [iter0, iter0 + T), one launch: one thread per (t, p, c) of the
+// hyper variates {hyper z, Gamma((G-1)/2)} (Marsaglia-Tsang on the Philox stream, or
+// gammainccinv of the replayed uniform) and per (t, p, g, c) of the step variates {z,
+// log u} (nmc_step_variate).  The hyper elements come first in the index space: their
+// rejection loops are the longest threads and, started first, run under the bulk of the
+// step elements.  (Two kernels -- the step one at 92 VGPRs -- measured no faster: on one
+// stream they run back to back, and a side stream for the Gamma draws did not overlap
+// them but added a join, profiles/r03h_*.)  The ring holds at most 1 GiB, so every element
+// index fits 32 bits.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) nmc_k_fill(Dev d, int iter0, int T) {
   const unsigned C = (unsigned)d.C, GC = (unsigned)d.G * C, PGC = (unsigned)d.P * GC;
+  const unsigned PC = (unsigned)d.P * C;
   const unsigned n1 = d.zin ? 0u : (unsigned)T * PGC;   // (zin: the step kernel draws these)
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n1; i += gridDim.x * blockDim.x) {
-    const unsigned t = i / PGC, r = i - t * PGC;
-    const unsigned p = r / GC, q = r - p * GC;
-    const unsigned g = q / C, c = q - g * C;
-    double z, lu;
-    nmc_step_variate(d, iter0 + (int)t, (int)p, (int)g, (int)c, z, lu);
-    d.vzl[2 * (size_t)i] = z;
-    d.vzl[2 * (size_t)i + 1] = lu;
-  }
-}
-
-__global__ void __launch_bounds__(256) nmc_k_fill_hyper(Dev d, int iter0, int T) {
-  const unsigned C = (unsigned)d.C, PC = (unsigned)d.P * C;
-  const unsigned n2 = (unsigned)T * PC;
-  for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < n2; j += gridDim.x * blockDim.x) {
-    const unsigned t = j / PC, r = j - t * PC;
-    const unsigned p = r / C, c = r - p * C;
-    const int it = iter0 + (int)t;
-    double hz, hx;
-    if (d.rng_mode == NMC_RNG_REPLAY) {
-      const size_t k = (size_t)it * PC + r;
-      hz = it < d.replay_n ? d.rhz[k] : nmc_nan();
-      hx = it < d.replay_n ? nmc_igamci(d.ha, d.rhu[k], d.hlga) : nmc_nan();
-    } else {
-      const uint32_t ch = (uint32_t)(d.chain_base + (int)c);
-      hz = nmc_normal(it, 0, p, NMC_PURPOSE_HYPER_NORMAL, ch, d.seed);
-      hx = nmc_gamma_mt(d.ha, it, p, ch, d.seed);
+  const unsigned n2 = d.pooling == NMC_POOL_PARTIAL ? (unsigned)T * PC : 0u;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n1 + n2;
+       i += gridDim.x * blockDim.x) {
+    if (i >= n2) {   // step element i - n2
+      const unsigned e = i - n2;
+      const unsigned t = e / PGC, r = e - t * PGC;
+      const unsigned p = r / GC, q = r - p * GC;
+      const unsigned g = q / C, c = q - g * C;
+      double z, lu;
+      nmc_step_variate(d, iter0 + (int)t, (int)p, (int)g, (int)c, z, lu);
+      d.vzl[2 * (size_t)e] = z;
+      d.vzl[2 * (size_t)e + 1] = lu;
+    } else {         // hyper element i
+      const unsigned t = i / PC, r = i - t * PC;
+      const unsigned p = r / C, c = r - p * C;
+      const int it = iter0 + (int)t;
+      double hz, hx;
+      if (d.rng_mode == NMC_RNG_REPLAY) {
+        const size_t k = (size_t)it * PC + r;
+        hz = it < d.replay_n ? d.rhz[k] : nmc_nan();
+        hx = it < d.replay_n ? nmc_igamci(d.ha, d.rhu[k], d.hlga) : nmc_nan();
+      } else {
+        const uint32_t ch = (uint32_t)(d.chain_base + (int)c);
+        hz = nmc_normal(it, 0, p, NMC_PURPOSE_HYPER_NORMAL, ch, d.seed);
+        hx = nmc_gamma_mt(d.ha, it, p, ch, d.seed);
+      }
+      d.vh[2 * (size_t)i] = hz;
+      d.vh[2 * (size_t)i + 1] = hx;
     }
-    d.vh[2 * (size_t)j] = hz;
-    d.vh[2 * (size_t)j + 1] = hx;
   }
 }
 

@@ -251,9 +251,6 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) { delete x; return fail(-2, std::string("hipSetDevice: ") + hipGetErrorString(e)); }
   e = hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->side, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&x->join, hipEventDisableTiming);
   if (e != hipSuccess) { nmc_destroy(x); return fail(-2, std::string("hipStreamCreate: ") + hipGetErrorString(e)); }
   for (auto& ev : x->ev) hipEventCreate(&ev);
 
@@ -441,15 +438,11 @@ int nmc_destroy(nmc_ctx* x) {
   if (!x) return 0;
   hipSetDevice(x->device);
   if (x->stream) hipStreamSynchronize(x->stream);
-  if (x->side) hipStreamSynchronize(x->side);
   for (void* p : x->owned) if (p) hipFree(p);
   for (auto& ev : x->ev) if (ev) hipEventDestroy(ev);
   for (auto& pr : x->kev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   for (auto& pr : x->hev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   if (x->stream) hipStreamDestroy(x->stream);
-  if (x->side) hipStreamDestroy(x->side);
-  if (x->fork) hipEventDestroy(x->fork);
-  if (x->join) hipEventDestroy(x->join);
   if (x->tmo_host) hipHostFree((void*)x->tmo_host);
   delete x;
   return 0;
@@ -622,29 +615,15 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
         x->launch_iters > 0 && x->launch_iters < x->d.vcap ? x->launch_iters : x->d.vcap;
     for (int c0 = iter_begin; c0 < iter_end; c0 += chunk) {
       const int c1 = c0 + chunk < iter_end ? c0 + chunk : iter_end;
-      // every variate of iterations [c0, c1): the hyper variates (partial pooling), then
-      // the step variates (unless the step kernel draws them), each one parallel launch
+      // every variate of iterations [c0, c1) in one fully parallel launch: the hyper
+      // variates (partial pooling) and the step variates (unless the step kernel draws them)
       x->d.vbase = c0;
-      auto blocks_for = [](size_t n) { return (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384); };
-      const size_t nh = partial ? (size_t)(c1 - c0) * P * x->C : 0;
-      const size_t ns = x->d.zin ? 0 : (size_t)(c1 - c0) * P * x->C * x->G;
-      // (the hyper fill -- a few latency-bound Gamma draws -- runs on the side stream,
-      // concurrently with the step-variate fill; it waits for everything queued before it,
-      // so it never overwrites variates a running step kernel still reads)
-      if (nh) {
-        HIPCHK(hipEventRecord(x->fork, x->stream));
-        HIPCHK(hipStreamWaitEvent(x->side, x->fork, 0));
-        hipLaunchKernelGGL(nmc_k_fill_hyper, dim3(blocks_for(nh)), dim3(256), 0, x->side, x->d,
-                           c0, c1 - c0);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(x->join, x->side));
-      }
-      if (ns) {
-        hipLaunchKernelGGL(nmc_k_fill, dim3(blocks_for(ns)), dim3(256), 0, x->stream, x->d, c0,
-                           c1 - c0);
+      const size_t n = (size_t)(c1 - c0) * P * x->C * ((x->d.zin ? 0 : x->G) + (partial ? 1 : 0));
+      if (n) {
+        const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);
+        hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);
         HIPCHK(hipGetLastError());
       }
-      if (nh) HIPCHK(hipStreamWaitEvent(x->stream, x->join, 0));
       // counters continue from the earlier launches (Dev.pbase / xbase): reset only
       // before they could wrap
       const uint64_t steps = (uint64_t)(c1 - c0) * P;
