@@ -213,6 +213,9 @@ enum { NMC_RUN_HYPER_LOAD = 1 };
 #ifndef NMC_GIBBS_TILES
 #define NMC_GIBBS_TILES 0
 #endif
+#ifndef NMC_TILE_TAPER
+#define NMC_TILE_TAPER 0
+#endif
 // Likelihood tiles per group (nmc_tiles) = partial-sum slots per accumulator.
 #ifndef NMC_NSLOT_N
 #define NMC_NSLOT_N 16
@@ -1074,6 +1077,17 @@ __device__ __forceinline__ nmc_tiling nmc_tiles(int n, int tile) {
   T.a = T.b = per;
   T.nt = (n + per - 1) / per;
   T.h = T.nt;
+#if NMC_TILE_TAPER   // (A/B build option) the queue's last tiles smaller: h tiles of 5/4 the
+                     // size, then tiles of 3/4, so the last waves to finish wait less
+  if (T.nt >= 8) {
+    const int a = ((per * 5 / 4) + 15) & ~15, b = ((per * 3 / 4) + 15) & ~15;
+    const int h = T.nt / 2;
+    const int rest = n - h * a;
+    if (b > 0 && rest > 0 && h + (rest + b - 1) / b <= NMC_NSLOT) {
+      T.a = a; T.b = b; T.h = h; T.nt = h + (rest + b - 1) / b;
+    }
+  }
+#endif
   return T;
 }
 
