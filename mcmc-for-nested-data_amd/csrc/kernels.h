@@ -216,6 +216,9 @@ enum { NMC_RUN_HYPER_LOAD = 1 };
 #ifndef NMC_TILE_TAPER
 #define NMC_TILE_TAPER 0
 #endif
+#ifndef NMC_HYPER_ALLP
+#define NMC_HYPER_ALLP 0
+#endif
 // Likelihood tiles per group (nmc_tiles) = partial-sum slots per accumulator.
 #ifndef NMC_NSLOT_N
 #define NMC_NSLOT_N 16
@@ -1909,8 +1912,8 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       // Gibbs update of parameter p after iteration t-1 at step (t, p), right before the
       // decision that needs it (all-wave modes: persistent SYNC, launch per iteration):
       // the publications it waits for are a whole step old
-      const bool hyper_now =
-          !hl && PARTIAL && t > 0 && !(t == i0 && (flags & NMC_RUN_HYPER_LOAD));
+      const bool hyper_now = !hl && PARTIAL && (NMC_HYPER_ALLP ? p == 0 : true) && t > 0 &&
+                             !(t == i0 && (flags & NMC_RUN_HYPER_LOAD));
       // persistent Gibbs wave: the Gibbs update of parameter q after iteration tq is
       // task k = tq*P + q; every workgroup publishes it right after its decision at
       // global step k, so it is counted at the start of step k+1.  P == 1: the Gibbs
@@ -2087,12 +2090,14 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       double verdict = 0.0;
       if constexpr (hl) if (aux_now) verdict = lds[L.flag * 64 + 1];
       if constexpr (PARTIAL && !hl) if (hyper_now) {
+        // (NMC_HYPER_ALLP: every parameter at step 0, once P-1's count is full)
+        const int hp = NMC_HYPER_ALLP ? -1 : p, wp = NMC_HYPER_ALLP ? P - 1 : p;
         if constexpr (sync) {   // parameter p of t-1 is published once its count is full
-          ok = nmc_wait_published(d, cb, p, (unsigned)G * (unsigned)(t - i0), lds, L);
+          ok = nmc_wait_published(d, cb, wp, (unsigned)G * (unsigned)(t - i0), lds, L);
           if (!ok) break;
-          nmc_hyper<NMC_SRC_SC1>(d, ((t - 1) & 1) ? d.vb1 : d.vb0, cb, t - 1, lds, L, g0w, p);
+          nmc_hyper<NMC_SRC_SC1>(d, ((t - 1) & 1) ? d.vb1 : d.vb0, cb, t - 1, lds, L, g0w, hp);
         } else {
-          nmc_hyper<NMC_SRC_GLOBAL>(d, ((t - 1) & 1) ? d.vb1 : d.vb0, cb, t - 1, lds, L, g0w, p);
+          nmc_hyper<NMC_SRC_GLOBAL>(d, ((t - 1) & 1) ? d.vb1 : d.vb0, cb, t - 1, lds, L, g0w, hp);
         }
         if (ctl) {
           const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];

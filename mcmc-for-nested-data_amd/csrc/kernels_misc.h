@@ -15,7 +15,10 @@
 // them but added a join, profiles/r03h_*.)  The ring holds at most 1 GiB, so every element
 // index fits 32 bits.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) nmc_k_fill(Dev d, int iter0, int T) {
+#ifndef NMC_FILL_MINB
+#define NMC_FILL_MINB 1
+#endif
+__global__ void __launch_bounds__(256, NMC_FILL_MINB) nmc_k_fill(Dev d, int iter0, int T) {
   const unsigned C = (unsigned)d.C, GC = (unsigned)d.G * C, PGC = (unsigned)d.P * GC;
   const unsigned PC = (unsigned)d.P * C;
   const unsigned n1 = d.zin ? 0u : (unsigned)T * PGC;   // (zin: the step kernel draws these)
