@@ -266,14 +266,19 @@ def main():
     kt = eng.kernel_timing()
     eng.set_kernel_timing(False)
 
-    gather_ms = None
+    gather_ms, gather_err = None, None
     if world > 1 and not args.no_gather:
-        comm = parallel.rccl_comm(pg, world, rank, device)
-        tg = time.perf_counter()
-        full = parallel.gather_samples(eng, comm, root=0)
-        gather_ms = (time.perf_counter() - tg) * 1e3
-        parallel.rccl_destroy(comm)
-        del full
+        # after the timed region: the one RCCL gather of the sample stores; a
+        # failure here is reported in the line, never lost with it
+        try:
+            comm = parallel.rccl_comm(pg, world, rank, device)
+            tg = time.perf_counter()
+            full = parallel.gather_samples(eng, comm, root=0)
+            gather_ms = (time.perf_counter() - tg) * 1e3
+            parallel.rccl_destroy(comm)
+            del full
+        except Exception as e:
+            gather_err = repr(e)
 
     C, G, N, P = args.chains, args.groups, args.obs, fam.n_params
     units = world * C * G * K
@@ -360,6 +365,7 @@ def main():
             "enqueue_ms": t_enq * 1e3,
             "hyper_only_avg_us": (kt["hyper_ms"] / max(1, kt["hyper_launches"])) * 1e3,
             "gather_ms": gather_ms,
+            "gather_error": gather_err,
         }
         print(json.dumps(out))
     eng.close()

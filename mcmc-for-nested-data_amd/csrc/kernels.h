@@ -216,8 +216,12 @@ enum { NMC_RUN_HYPER_LOAD = 1 };
 #ifndef NMC_TILE_TAPER
 #define NMC_TILE_TAPER 0
 #endif
+// All-wave Gibbs modes (SYNC, LAUNCH): update every parameter after iteration t-1 at
+// step 0 of t (1), or parameter p at step (t, p) (0: waits for a publication one step old,
+// but runs two updates per iteration; measured 53.8-53.9 against 51.8-52.2 us/iter at the
+// cfg-4 shard, profiles/r03j_ab_allp.json)
 #ifndef NMC_HYPER_ALLP
-#define NMC_HYPER_ALLP 0
+#define NMC_HYPER_ALLP 1
 #endif
 // Likelihood tiles per group (nmc_tiles) = partial-sum slots per accumulator.
 #ifndef NMC_NSLOT_N
@@ -1909,9 +1913,9 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       // cannot change before the decision), so only the slot sum, finish and the
       // Metropolis test remain between the barriers
       typename Fam::Reg c_reg{};
-      // Gibbs update of parameter p after iteration t-1 at step (t, p), right before the
-      // decision that needs it (all-wave modes: persistent SYNC, launch per iteration):
-      // the publications it waits for are a whole step old
+      // Gibbs update after iteration t-1 in the all-wave modes (persistent SYNC, launch per
+      // iteration): every parameter at step 0 of t (NMC_HYPER_ALLP), or parameter p at step
+      // (t, p), right before the decision that needs it
       const bool hyper_now = !hl && PARTIAL && (NMC_HYPER_ALLP ? p == 0 : true) && t > 0 &&
                              !(t == i0 && (flags & NMC_RUN_HYPER_LOAD));
       // persistent Gibbs wave: the Gibbs update of parameter q after iteration tq is
