@@ -220,6 +220,9 @@ enum { NMC_RUN_HYPER_LOAD = 1 };
 // step 0 of t (1), or parameter p at step (t, p) (0: waits for a publication one step old,
 // but runs two updates per iteration; measured 53.8-53.9 against 51.8-52.2 us/iter at the
 // cfg-4 shard, profiles/r03j_ab_allp.json)
+#ifndef NMC_GIBBS_ON_CTL
+#define NMC_GIBBS_ON_CTL 0
+#endif
 #ifndef NMC_HYPER_ALLP
 #define NMC_HYPER_ALLP 1
 #endif
@@ -1594,7 +1597,10 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const size_t PGC = (size_t)P * G * C;
   const size_t gc = (size_t)g * C + cc;
   const bool ctl = w == 0;
-  const bool gw = hl && w == 1;                   // the Gibbs wave
+  // NMC_GIBBS_ON_CTL (build option): the register hand-off's Gibbs task runs on the control
+  // wave at the start of each step, so wave 1 takes likelihood tiles like the others
+  constexpr bool gmerge = MODE == NMC_MODE_SYNC_REG && NMC_GIBBS_ON_CTL;
+  const bool gw = hl && w == 1 && !gmerge;        // the Gibbs wave
   // latency-bound roles (control, Gibbs) issue ahead of the waves sharing their SIMD
   if (W > 1 && (ctl || gw) && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
 
@@ -1849,37 +1855,42 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     nmc_drain_vm();
     return;
   }
-  if constexpr (hr && !own) if (gw) {
+  // the register hand-off's task of step (t, p): task k = gs - lag = (kt, kq) -- poll, fetch,
+  // update, and (P <= 2) this step's priors; lane 0 leaves the verdict in the flag word
+  auto gibbs_step = [&](int t, int p) {
+    const int gs = t * P + p;
+    if (gs - lag < i0 * P) return;
+    const int k = gs - lag, kq = k % P, kt = k / P;
+    const bool r = nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1));
+    if (lane == 0)
+      __hip_atomic_store(lds + L.flag * 64 + 1, r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (p == 0) NMC_STAMP_AUX(t, 13);
+    if (r) {
+      // keep the payload loads below the poll (no instruction: wavefront scope)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      nmc_hyper_update_reg<false>(d, cb, kt, kq, cc, lds, L.hyp, g0w);
+      if (p == 0) NMC_STAMP_AUX(t, 15);
+      if (P <= 2) {   // the update lands in the step that needs it: this step's priors
+        const int sp = gs & 1;
+        const double v = th[p * 64];
+        const double prop = v + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
+                                    lds[(L.zl + 2 * sp) * 64 + 2 * lane];
+        const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
+        const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
+        cwv[NMC_CW_LPC * 64] =
+            t > 0 ? nmc_norm_logpdf_r(v, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
+        cwv[NMC_CW_LPP * 64] = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
+      }
+    }
+  };
+  if constexpr (hr && !own && !gmerge) if (gw) {
     const int gs0 = i0 * P;
     for (int t = i0; t < i1 && ok; ++t) {
       for (int p = 0; p < P; ++p) {
         const int gs = t * P + p;
         const bool due = gs - lag >= gs0;
-        if (due) {   // task k = gs - lag = (kt, kq): poll, fetch, update
-          const int k = gs - lag, kq = k % P, kt = k / P;
-          const bool r = nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1));
-          if (lane == 0)
-            __hip_atomic_store(lds + L.flag * 64 + 1, r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (p == 0) NMC_STAMP_AUX(t, 13);
-          if (r) {
-            // keep the payload loads below the poll (no instruction: wavefront scope)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            nmc_hyper_update_reg<false>(d, cb, kt, kq, cc, lds, L.hyp, g0w);
-            if (p == 0) NMC_STAMP_AUX(t, 15);
-            if (P <= 2) {   // the update lands in the step that needs it: this step's priors
-              const int sp = gs & 1;
-              const double v = th[p * 64];
-              const double prop = v + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
-                                          lds[(L.zl + 2 * sp) * 64 + 2 * lane];
-              const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
-              const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
-              cwv[NMC_CW_LPC * 64] =
-                  t > 0 ? nmc_norm_logpdf_r(v, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
-              cwv[NMC_CW_LPP * 64] = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
-            }
-          }
-        }
+        gibbs_step(t, p);
 #if NMC_GIBBS_TILES   // (A/B build option: the Gibbs wave takes likelihood tiles after its task)
         lik_tiles(t, p, gs & 1, [] {});
 #endif
@@ -2067,6 +2078,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         if (tn < i1 && !(NMC_ZIN_BUILD && d.zin)) put_zl(tn, pn, sp ^ 1);   // (zin: the job)
             };
       bool ctl_done = !ctl;
+      if constexpr (gmerge) if (ctl) gibbs_step(t, p);
       if (ctl) {
         ctl_work();
         ctl_done = true;
@@ -2205,6 +2217,8 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     const int wk = hr && !own ? close_k : ge - 1;   // the task whose publication is awaited
     const bool pub = nmc_wait_published(d, cb, wk % P, (unsigned)G * (unsigned)(wk / P - i0 + 1),
                                         lds, L);
+    if constexpr (gmerge) if (pub && ctl)   // (the closing task of the merged Gibbs role)
+      nmc_hyper_update_reg<false>(d, cb, close_k / P, close_k % P, cc, lds, L.hyp, true);
     if (!hr && pub && gw) {
       const double* src = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
       const int ho = ((ge - 1) & 1) * (G + 1);
