@@ -220,9 +220,6 @@ enum { NMC_RUN_HYPER_LOAD = 1 };
 // step 0 of t (1), or parameter p at step (t, p) (0: waits for a publication one step old,
 // but runs two updates per iteration; measured 53.8-53.9 against 51.8-52.2 us/iter at the
 // cfg-4 shard, profiles/r03j_ab_allp.json)
-#ifndef NMC_GIBBS_ON_CTL
-#define NMC_GIBBS_ON_CTL 0
-#endif
 #ifndef NMC_HYPER_ALLP
 #define NMC_HYPER_ALLP 1
 #endif
@@ -1597,10 +1594,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
   const size_t PGC = (size_t)P * G * C;
   const size_t gc = (size_t)g * C + cc;
   const bool ctl = w == 0;
-  // NMC_GIBBS_ON_CTL (build option): the register hand-off's Gibbs task runs on the control
-  // wave at the start of each step, so wave 1 takes likelihood tiles like the others
-  constexpr bool gmerge = MODE == NMC_MODE_SYNC_REG && NMC_GIBBS_ON_CTL;
-  const bool gw = hl && w == 1 && !gmerge;        // the Gibbs wave
+  const bool gw = hl && w == 1;                   // the Gibbs wave
   // latency-bound roles (control, Gibbs) issue ahead of the waves sharing their SIMD
   if (W > 1 && (ctl || gw) && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
 
@@ -1884,7 +1878,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       }
     }
   };
-  if constexpr (hr && !own && !gmerge) if (gw) {
+  if constexpr (hr && !own) if (gw) {
     const int gs0 = i0 * P;
     for (int t = i0; t < i1 && ok; ++t) {
       for (int p = 0; p < P; ++p) {
@@ -2078,7 +2072,6 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
         if (tn < i1 && !(NMC_ZIN_BUILD && d.zin)) put_zl(tn, pn, sp ^ 1);   // (zin: the job)
             };
       bool ctl_done = !ctl;
-      if constexpr (gmerge) if (ctl) gibbs_step(t, p);
       if (ctl) {
         ctl_work();
         ctl_done = true;
@@ -2217,8 +2210,6 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     const int wk = hr && !own ? close_k : ge - 1;   // the task whose publication is awaited
     const bool pub = nmc_wait_published(d, cb, wk % P, (unsigned)G * (unsigned)(wk / P - i0 + 1),
                                         lds, L);
-    if constexpr (gmerge) if (pub && ctl)   // (the closing task of the merged Gibbs role)
-      nmc_hyper_update_reg<false>(d, cb, close_k / P, close_k % P, cc, lds, L.hyp, true);
     if (!hr && pub && gw) {
       const double* src = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
       const int ho = ((ge - 1) & 1) * (G + 1);
