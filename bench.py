@@ -1,22 +1,33 @@
 #!/usr/bin/env python
 """Benchmark: MCMC iterations of the nested-data sampler on MI355X.
 
-Workload (BASELINE.json configs[2], SURVEY 8(d) cfg 3), per GPU: partial-pooling
-linear regression (sigma = 1 known, 2 parameters per group), 256 chains x 64
-groups x 1000 observations, synthetic data from RandomState(7).  One step = one
-full reference iteration (Sampler._loop body: both parameters' Metropolis steps
-over every (chain, group) + both Gibbs hyper updates + recording).
+Workloads (BASELINE.json configs); ``--workload`` picks one, default cfg3:
 
-value = chains x groups x iterations / second over the whole job (weak scaling:
-each rank runs its own 256 chains, global chain ids rank*256.., no collective in
-the loop; one RCCL gather of the sample stores after the timed region).
+  cfg3  (the headline)  partial-pooling linear regression (sigma = 1 known, 2 parameters
+        per group), 256 chains x 64 groups x 1000 observations PER GPU, synthetic data
+        from RandomState(7); weak scaling (rank r runs global chains r*256..).
+  cfg2  no-pooling Gaussian means (example.distribution), 256 chains x 32 groups x 500
+        observations per GPU, 3 parameters; weak scaling.
+  cfg4  partial-pooling regression, 1024 chains x 256 groups x 2000 observations IN TOTAL,
+        sharded over the N ranks (128 per rank at N = 8); strong scaling.
+  cfg5  partial pooling with the user-supplied 8-parameter logistic log-likelihood (a
+        runtime-compiled DeviceLikelihood), 512 chains x 128 groups x 5000 observations in
+        total, sharded over the N ranks; strong scaling.
 
-Launch:  python bench.py [--gpus N --steps K --warmup W]
-         (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py)
+One step = one full reference iteration (Sampler._loop body: every parameter's
+Metropolis step over every (chain, group), the Gibbs hyper updates under partial
+pooling, recording).  value = chains x groups x iterations / second over the whole job
+(max over ranks of the timed region); no collective in the loop, one RCCL gather of the
+sample stores after the timed region.
+
+Launch:  python bench.py [--workload cfg3] [--gpus N --steps K --warmup W]
+         (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py; the host
+         bootstrap is nestmc.parallel.HostGroup, no PyTorch)
 """
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -33,24 +44,65 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # fp64 VALU issue: 256 CUs x 4 SIMDs x 16 fp64 lanes x 2.4 GHz lane-instructions per second
 # (the 78.6 TFLOP/s fp64 vector peak counts an FMA as 2 flops)
 VALU_PEAK_TIPS = 256 * 4 * 16 * 2.4e9 / 1e12
-VALU_PER_CHAIN_ROW = 3          # fp64 VALU lane-instructions per (chain, row, parameter step)
+LDS_PEAK_GBS = 256.0 * 256 * 2.4   # 256 B/clk/CU (ds_read_b64/b128) x 256 CUs x 2.4 GHz
+
+# fp64 VALU lane-instructions the shipped row loop issues per (chain, row, parameter step),
+# by the family instance in the step kernel's name -- counted in the ISA of that loop
+# (profiles/isa_*):
+#   FamLinreg<2>     {x, y} rows: b0 - y (add), fma(x, b1, .), fma(e, e, acc) = 3, in the
+#                    paired asm loop (24 per 8-row block for two chains per lane), the
+#                    broadcast asm loop and the C++ loop alike
+#   FamGaussMean<F>  per field: theta - m (add), fma(e, e, acc) = 2F
+VALU_PER_CHAIN_ROW = {"FamLinreg<2>": 3, "FamGaussMean<3>": 6}
+
+LOGISTIC8 = r"""
+__device__ double nmc_user_loglik(const double* th, const double* row, const double* k) {
+  double eta = th[0];
+  for (int j = 0; j < 7; ++j) eta = fma(row[j], th[j + 1], eta);
+  return row[7] * eta - nmc_logaddexp0(eta);
+}
+"""
+
+WORKLOADS = {
+    "cfg3": dict(kind="linreg", chains=256, groups=64, obs=1000, pooling="partial",
+                 scaling="weak",
+                 desc="cfg3 partial-pooling linear regression (sigma=1), %d chains x %d groups "
+                      "x %d obs per GPU, P=%d"),
+    "cfg2": dict(kind="gauss", chains=256, groups=32, obs=500, pooling="none", scaling="weak",
+                 desc="cfg2 no-pooling Gaussian means (example.distribution), %d chains x %d "
+                      "groups x %d obs per GPU, P=%d"),
+    "cfg4": dict(kind="linreg", chains=1024, groups=256, obs=2000, pooling="partial",
+                 scaling="strong",
+                 desc="cfg4 partial-pooling linear regression (sigma=1), %d chains in total x "
+                      "%d groups x %d obs sharded over the GPUs, P=%d"),
+    "cfg5": dict(kind="user_logistic", chains=512, groups=128, obs=5000, pooling="partial",
+                 scaling="strong",
+                 desc="cfg5 partial pooling, user-supplied logistic log-likelihood "
+                      "(DeviceLikelihood, hiprtc), %d chains in total x %d groups x %d obs "
+                      "sharded over the GPUs, P=%d"),
+}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg3")
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--chains", type=int, default=256, help="chains per GPU")
-    ap.add_argument("--groups", type=int, default=64)
-    ap.add_argument("--obs", type=int, default=1000)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0,
-                    help="budget for the CPU baseline sample (0 disables)")
+    ap.add_argument("--chains", type=int, default=None,
+                    help="chains per GPU (weak workloads) or in total (strong ones)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="timed window of the CPU baseline sample (0 disables)")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the two rocprofv3 PMC passes that measure HBM traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    return ap.parse_args()
+    a = ap.parse_args()
+    wl = dict(WORKLOADS[a.workload])
+    if a.chains:
+        wl["chains"] = a.chains
+    a.wl = wl
+    return a
 
 
 def dist_env():
@@ -60,47 +112,154 @@ def dist_env():
     return world, rank, local
 
 
-def make_engine(args, rank, device):
-    from nestmc.engine import Engine
-    from nestmc.families import LinearRegression
+def rank_chains(wl, world, rank):
+    """(first global chain id, count) of this rank: weak workloads run ``chains`` per rank,
+    strong ones split the total (nestmc.parallel.shard, contiguous blocks)."""
+    from nestmc.parallel import shard
+    if wl["scaling"] == "weak":
+        return rank * wl["chains"], wl["chains"]
+    return shard(wl["chains"], world, rank)
+
+
+def make_problem(wl):
+    """(family, names, priors, ranges) of a workload, data regenerated from its seed."""
+    import scipy.stats
     from nestmc import data
+    from nestmc.families import DeviceLikelihood, GaussianMean, LinearRegression, Logistic
+    G, N = wl["groups"], wl["obs"]
+    if wl["kind"] == "linreg":
+        x, y, _, _ = data.linreg(G, N, seed=7)
+        return (LinearRegression.simple(x, y, sigma=1.0), ("b0", "b1"), None,
+                {"b0": [-1, 1], "b1": [0, 3]})
+    if wl["kind"] == "gauss":
+        mu, sd = data.example_distribution(3, G)
+        return (GaussianMean.from_groups(mu, sd, [N] * G), ("a", "b", "c"),
+                [scipy.stats.norm(0, 1)] * 3, None)
+    X, y, _ = data.logistic(G, N, n_coef=8, seed=1)
+    host = Logistic(X, y)
+    fam = DeviceLikelihood(host.obs(), LOGISTIC8, 8, host_function=host)
+    names = tuple("b%d" % j for j in range(8))
+    return fam, names, None, {n: [-0.5, 0.5] for n in names}
+
+
+def make_engine(wl, rank, world, device):
+    from nestmc.engine import Engine
     from nestmc.init import init_chains
-    G, N, C = args.groups, args.obs, args.chains
-    x, y, _, _ = data.linreg(G, N, seed=7)
-    fam = LinearRegression.simple(x, y, sigma=1.0)
+    fam, names, priors, ranges = make_problem(wl)
+    G, N = wl["groups"], wl["obs"]
     sizes = [N] * G
-    chains = range(rank * C, (rank + 1) * C)
-    eng = Engine(fam, sizes, C, "partial", seed=1234, chain_base=rank * C, device=device)
-    # reference-order init of every chain (start point uniform in the example ranges),
-    # likelihoods batched on the device; outside the timed region
-    st = init_chains(fam, sizes, ("b0", "b1"), chains, "partial", None,
-                     {"b0": [-1, 1], "b1": [0, 3]}, False, group_ll=eng.eval_group_ll)
+    c0, C = rank_chains(wl, world, rank)
+    eng = Engine(fam, sizes, C, wl["pooling"], priors, seed=1234, chain_base=c0,
+                 device=device)
+    # reference-order init of every chain (start point uniform in the example ranges /
+    # drawn from the priors), likelihoods batched on the device; outside the timed region
+    st = init_chains(fam, sizes, names, range(c0, c0 + C), wl["pooling"], priors, ranges,
+                     False, threads=8, group_ll=eng.eval_group_ll)
     eng.set_state(st["value"], st["log_prior"], st["ll"], st["mu"], st["s2"])
-    return eng, fam
+    return eng, fam, C
 
 
-def cpu_baseline(args, budget_s):
-    """Time the numpy oracle (a restatement of the reference's per-chain loop, legacy
-    RNG, process per chain) on this host's cores over a bounded sample."""
+# ---------------------------------------------------------------------------------------
+# CPU baseline: the numpy oracle on this host's cores, loop-only timing
+# ---------------------------------------------------------------------------------------
+def _oracle_problem(wl):
+    """The workload for the oracle: (Nested, names, priors, ranges), the likelihood in the
+    reference's callable convention (parameter[P][n] -> ll[n])."""
+    from oracle import restatement as rs
+    from oracle.models import linreg_callback
+    from nestmc import data
+    G, N = wl["groups"], wl["obs"]
+    if wl["kind"] == "linreg":
+        # the reference's own callback form (example/regression.py:53-67, scipy norm)
+        x, y, _, _ = data.linreg(G, N, seed=7)
+        f, names, priors, ranges = (linreg_callback(x, y), ("b0", "b1"), None,
+                                    {"b0": [-1, 1], "b1": [0, 3]})
+    elif wl["kind"] == "gauss":
+        f, names, priors, ranges = make_problem(wl)     # GaussianMean is callable
+    else:
+        from nestmc.families import Logistic
+        X, y, _ = data.logistic(G, N, n_coef=8, seed=1)
+        names = tuple("b%d" % j for j in range(8))
+        f, priors, ranges = Logistic(X, y), None, {n: [-0.5, 0.5] for n in names}
+    return rs.Nested(f, [N] * G), names, priors, ranges
+
+
+_CPU = {}
+
+
+def _cpu_init(job):
+    """Pool worker: chain init (untimed), kept for the timed loop."""
+    wl, chain = job
+    from oracle import restatement as rs
+    nested, names, priors, ranges = _oracle_problem(wl)
+    st, r = rs.init_chain(nested, names, chain, wl["pooling"], priors, ranges, False)
+    _CPU[chain] = (nested, st, r, priors)
+    return chain
+
+
+def _cpu_loop(job):
+    """Pool worker: wait at the barrier, then time only the sampling loop (SURVEY 8(d):
+    init excluded).  Returns (start, end) in time.time() seconds."""
+    wl, chain, iters, barrier = job
+    from oracle import restatement as rs
+    nested, st, r, priors = _CPU[chain]
+    barrier.wait()
+    t0 = time.time()
+    rs.run(nested, st, wl["pooling"], priors, iters, iters, 1, rs.LegacyRNG(r))
+    return t0, time.time()
+
+
+def _cpu_worker(args):
+    (wl, chain, iters), barrier = args
+    _cpu_init((wl, chain))
+    return _cpu_loop((wl, chain, iters, barrier))
+
+
+def cpu_cores():
+    """Cores this process may run on (the affinity mask), capped by OMP_NUM_THREADS when the
+    host sets it (the GPU box gives each GPU a 16-core share and says so there)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n), len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(wl, window_s):
+    """The numpy oracle (a restatement of the reference's per-chain loop, legacy RNG, one
+    process per chain) on this host's cores: a probe sizes the sample so the timed loop
+    lasts ``window_s``; chain init is outside the timed window."""
     import multiprocessing as mp
-    cores = min(16, os.cpu_count() or 1)
-    # one probe iteration to size the sample
+    from oracle import restatement as rs
+    cores, affinity = cpu_cores()
+    # warm the imports and size the sample: init one chain, one untimed iteration, then
+    # time two
+    nested, names, priors, ranges = _oracle_problem(wl)
+    st, r = rs.init_chain(nested, names, 0, wl["pooling"], priors, ranges, False)
+    rs.run(nested, st, wl["pooling"], priors, 1, 1, 1, rs.LegacyRNG(r))
     t0 = time.time()
-    _cpu_chain((0, 1, args.groups, args.obs))
-    per_iter = max(time.time() - t0, 1e-3)
-    iters = max(2, int(budget_s / per_iter))
-    jobs = [(c, iters, args.groups, args.obs) for c in range(cores)]
-    t0 = time.time()
-    with mp.get_context("fork").Pool(cores) as pool:
-        pool.map(_cpu_chain, jobs)
-    wall = time.time() - t0
-    rate = cores * args.groups * iters / wall
+    rs.run(nested, st, wl["pooling"], priors, 3, 3, 1, rs.LegacyRNG(r), iter_begin=1)
+    per_iter = max((time.time() - t0) / 2.0, 1e-4)
+    iters = max(2, int(math.ceil(window_s / per_iter)))
+    ctx = mp.get_context("fork")
+    with ctx.Manager() as man:
+        barrier = man.Barrier(cores)
+        with ctx.Pool(cores) as pool:
+            spans = pool.map(_cpu_worker, [((wl, c, iters), barrier) for c in range(cores)],
+                             chunksize=1)
+    t_start = min(s for s, _ in spans)
+    t_end = max(e for _, e in spans)
+    wall = t_end - t_start
+    rate = cores * wl["groups"] * iters / wall
     out = {"value": rate, "unit": "chain*group*iter/s", "cores": cores, "kind": "port",
-           "sample": "%d chains x %d iterations of the cfg-3 workload (%d groups x %d obs, "
-                     "partial pooling) in the numpy oracle, one process per chain"
-                     % (cores, iters, args.groups, args.obs)}
+           "sample": "%d chains x %d iterations of the %s workload (%d groups x %d obs, %s "
+                     "pooling) in the numpy oracle, one process per chain on %d cores (affinity "
+                     "mask %d); timed loop only (init excluded): %.1f s"
+                     % (cores, iters, wl.get("name", "?"), wl["groups"], wl["obs"],
+                        wl["pooling"], cores, affinity, wall),
+           "timed_seconds": wall, "iterations": iters}
     cal = os.path.join(ROOT, "profiles", "cpu_calibration_r03.json")
-    if os.path.exists(cal):
+    if wl.get("name") == "cfg3" and os.path.exists(cal):
         # the reference cannot travel to this box: its speed relative to the restatement
         # was measured side by side in the build container (oracle/calibrate_cpu.py)
         ratio = json.load(open(cal))["reference_over_restatement"]
@@ -111,27 +270,14 @@ def cpu_baseline(args, budget_s):
     return out
 
 
-def _cpu_chain(job):
-    chain, iters, G, N = job
-    from nestmc import data
-    from oracle import restatement as rs
-    from oracle.models import linreg_callback
-    x, y, _, _ = data.linreg(G, N, seed=7)
-    nested = rs.Nested(linreg_callback(x, y), [N] * G)
-    st, r = rs.init_chain(nested, ("b0", "b1"), chain, "partial", None,
-                          {"b0": [-1, 1], "b1": [0, 3]}, False)
-    rs.run(nested, st, "partial", None, iters, iters, 1, rs.LegacyRNG(r))
-    return chain
-
-
-LDS_PEAK_GBS = 256.0 * 256 * 2.4   # 256 B/clk/CU (ds_read_b64/b128) x 256 CUs x 2.4 GHz
-
-
+# ---------------------------------------------------------------------------------------
+# HBM traffic: two rocprofv3 PMC passes of this script's K-iteration launch
+# ---------------------------------------------------------------------------------------
 def pmc_child(args):
     """Runs under rocprofv3 --pmc: the same workload and launches as the timed region
     (warmup launch of W iterations, then one launch of K iterations)."""
     from nestmc import _lib
-    eng, _ = make_engine(args, 0, 0)
+    eng, _, _ = make_engine(args.wl, 0, 1, 0)
     W, K = args.warmup, args.steps
     eng.set_schedule(W + K, (W + K) // 2, 1)
     eng.run(0, W)
@@ -160,9 +306,9 @@ def measure_traffic(args):
             d = os.path.join(base, counter)
             cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc",
                    "--", "python3", os.path.abspath(__file__), "--pmc-child",
+                   "--workload", args.workload,
                    "--steps", str(args.steps), "--warmup", str(args.warmup),
-                   "--chains", str(args.chains), "--groups", str(args.groups),
-                   "--obs", str(args.obs)]
+                   "--chains", str(args.wl["chains"])]
             p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
                                  stderr=subprocess.DEVNULL, start_new_session=True)
             try:
@@ -195,8 +341,17 @@ def measure_traffic(args):
                       "script's K-iteration launch; FETCH_SIZE x2 (gfx950), KiB -> bytes"}
 
 
+def fam_instance(kernel):
+    """'FamLinreg<2>' out of 'nmc_k_run<FamLinreg<2>, NMC_MODE_..., true>'."""
+    i = kernel.find("<")
+    j = kernel.find(">", i + 1)
+    return kernel[i + 1:j + 1] if i >= 0 and j > i else kernel
+
+
 def main():
     args = parse()
+    wl = args.wl
+    wl["name"] = args.workload
     world, rank, local = dist_env()
     if args.pmc_child:
         return pmc_child(args)
@@ -213,21 +368,17 @@ def main():
                 pmc = {"error": repr(e)}
         if args.cpu_seconds > 0:
             try:
-                cpu = cpu_baseline(args, args.cpu_seconds)
+                cpu = cpu_baseline(wl, args.cpu_seconds)
             except Exception as e:
                 cpu = {"value": None, "error": repr(e)}
-    pg = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
-        pg = dist
     from nestmc import _lib
     from nestmc import parallel
+    hg = parallel.HostGroup(world, rank) if world > 1 else None
 
     n_dev = _lib.device_count()
     assert n_dev >= 1, "no HIP device visible"
     device = local % n_dev
-    eng, fam = make_engine(args, rank, device)
+    eng, fam, C = make_engine(wl, rank, world, device)
     K, W = args.steps, args.warmup
     n_iter = W + 2 * K
     # schedule: record the second half like the reference (burn = n_iter // 2)
@@ -240,8 +391,8 @@ def main():
     eng.synchronize()
 
     def barrier():
-        if pg is not None:
-            pg.barrier()
+        if hg is not None:
+            hg.barrier()
 
     # timed region: exactly K iterations
     barrier()
@@ -257,7 +408,8 @@ def main():
     wall = t1 - t0
     ev_ms = eng.event_elapsed_ms(0, 1)
     t_rank = max(wall, ev_ms / 1e3)
-    t_max = parallel.max_over_ranks(t_rank, pg)
+    t_max = parallel.max_over_ranks(t_rank, hg)
+    c_total = C * world if wl["scaling"] == "weak" else wl["chains"]
 
     # second pass, same length: per-launch events on the engine's stream -> the
     # step kernel's average duration for the roofline
@@ -271,7 +423,7 @@ def main():
         # after the timed region: the one RCCL gather of the sample stores; a
         # failure here is reported in the line, never lost with it
         try:
-            comm = parallel.rccl_comm(pg, world, rank, device)
+            comm = parallel.rccl_comm(hg, world, rank, device)
             tg = time.perf_counter()
             full = parallel.gather_samples(eng, comm, root=0)
             gather_ms = (time.perf_counter() - tg) * 1e3
@@ -280,40 +432,42 @@ def main():
         except Exception as e:
             gather_err = repr(e)
 
-    C, G, N, P = args.chains, args.groups, args.obs, fam.n_params
-    units = world * C * G * K
+    G, N, P = wl["groups"], wl["obs"], fam.n_params
+    units = c_total * G * K
     value = units / t_max
     launches = kt["step_launches"]
     avg_step_ms = kt["step_ms"] / max(1, launches)
     iters_per_launch = kt["step_iters"] / max(1, launches)
     b_obs = fam.bytes_per_obs()
     lc = eng.launch_config()
+    kname = lc["kernel"]
+    inst = fam_instance(kname)
     # B_unit = P*N*b_obs per chain*group*iteration (each parameter step
-    # evaluates the group's rows once per chain).  The rows are LDS-resident for the
-    # launch, so these bytes never come from HBM; they are the rows delivered to the
-    # chain lanes.
+    # evaluates the group's rows once per chain), for THIS rank's chains per launch
     bytes_per_launch = C * G * P * N * b_obs * iters_per_launch
     achieved_gbs = bytes_per_launch / (avg_step_ms * 1e-3) / 1e9
-    # The binding resource is fp64 VALU issue.  The shipped row loop (kernels.h
-    # nmc_rows_lds_linreg2_paired; profiles/isa_r03_linreg_paired.txt) issues 24 fp64 VALU
-    # instructions (v_add_f64 x8, v_fma_f64 x16) per 8-row block for two chains per lane:
-    # 3 per (chain, row, parameter step) -- the whole likelihood work.  achieved = those
-    # lane-instructions per second; peak = 256 CUs x 4 SIMDs x 16 fp64 lanes x 2.4 GHz
-    # (= the 78.6 TFLOP/s fp64 vector peak / 2 flops per FMA).
-    lane_instr_per_launch = C * G * P * N * VALU_PER_CHAIN_ROW * iters_per_launch
-    valu_tips = lane_instr_per_launch / (avg_step_ms * 1e-3) / 1e12
-    # LDS bytes actually delivered: one ds_read_b128 serves a row pair to the 64 lanes, i.e.
-    # each (row, chain pair) once -- half the algorithmic bytes in the paired loop
-    lds_delivered = bytes_per_launch / (2.0 if lc.get("kernel", "").find("Linreg<2>") >= 0 else 1.0)
+    # The binding resource is fp64 VALU issue: the lane-instructions of the shipped row loop
+    # per (chain, row, parameter step), counted in its ISA for this family instance (null
+    # for an instance whose loop has not been counted)
+    per_row = VALU_PER_CHAIN_ROW.get(inst)
+    if per_row is not None:
+        lane_instr_per_launch = C * G * P * N * per_row * iters_per_launch
+        valu_tips = lane_instr_per_launch / (avg_step_ms * 1e-3) / 1e12
+    else:
+        lane_instr_per_launch, valu_tips = None, None
+    # LDS bytes actually delivered: the paired loop's ds_read_b128 serves a row pair to the
+    # 64 lanes, i.e. each (row, chain pair) once -- half the algorithmic bytes
+    paired = "Linreg<2>" in inst or "GaussMean" in inst
+    lds_delivered = bytes_per_launch / (2.0 if paired else 1.0)
     lds_gbs = lds_delivered / (avg_step_ms * 1e-3) / 1e9
     traffic, hbm_meas = None, None
     if pmc and "bytes_per_launch" in pmc:
         # measured for a K-iteration launch; scaled if this run's launches differ
         traffic = pmc["bytes_per_launch"] * iters_per_launch / pmc["iterations_per_launch"]
         hbm_meas = traffic / (avg_step_ms * 1e-3) / 1e9
-    kname = lc["kernel"]
 
     if rank == 0:
+        desc = wl["desc"] % (wl["chains"], G, N, P)
         out = {
             "metric": METRIC,
             "value": value,
@@ -323,32 +477,34 @@ def main():
             "warmup": W,
             "ms_per_step": t_max * 1e3 / K,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": wl["scaling"],
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": "cfg3 partial-pooling linear regression (sigma=1), "
-                                   "%d chains x %d groups x %d obs per GPU, P=%d" % (C, G, N, P),
-                       "chains_per_gpu": C, "groups": G, "obs_per_group": N, "params": P,
-                       "pooling": "partial", "parallelism": "chains sharded x%d" % world,
-                       "launch": lc},
+            "config": {"workload": desc, "name": args.workload,
+                       "chains_total": c_total, "chains_per_gpu": C, "groups": G,
+                       "obs_per_group": N, "params": P, "pooling": wl["pooling"],
+                       "parallelism": "chains sharded x%d" % world, "launch": lc},
             "roofline": {"bound": "valu", "achieved": valu_tips, "peak": VALU_PEAK_TIPS,
-                         "unit": "T fp64 lane-instr/s", "frac": valu_tips / VALU_PEAK_TIPS,
+                         "unit": "T fp64 lane-instr/s",
+                         "frac": None if valu_tips is None else valu_tips / VALU_PEAK_TIPS,
                          "traffic": traffic,
                          "kernel": kname,
                          "avg_launch_us": avg_step_ms * 1e3,
                          "iterations_per_launch": iters_per_launch,
+                         "valu_per_chain_row": per_row,
                          "valu_lane_instr_per_launch": lane_instr_per_launch,
-                         "derivation": "achieved = C*G*P*N*3 fp64 VALU lane-instructions per "
-                                       "iteration (the shipped paired row loop: 24 per 8-row "
-                                       "block per 2 chains) x iterations_per_launch / "
-                                       "avg_launch_us; peak = 256 CUs x 4 SIMDs x 16 fp64 lanes "
-                                       "x 2.4 GHz (78.6 TFLOP/s fp64 / 2)",
+                         "derivation": "achieved = C*G*P*N*valu_per_chain_row fp64 VALU "
+                                       "lane-instructions per iteration (the shipped row loop "
+                                       "of this family instance, counted in its ISA) x "
+                                       "iterations_per_launch / avg_launch_us (this rank's "
+                                       "chains); peak = 256 CUs x 4 SIMDs x 16 fp64 lanes x "
+                                       "2.4 GHz (78.6 TFLOP/s fp64 / 2)",
                          "lds": {"delivered_gbs": lds_gbs, "peak": LDS_PEAK_GBS,
                                  "frac": lds_gbs / LDS_PEAK_GBS,
-                                 "note": "bytes the ds_read_b128 of the paired loop deliver "
-                                         "(each serves a row pair to 64 lanes = 2 chains per "
-                                         "row): half of C*G*P*N*b_obs"},
+                                 "note": "bytes the row loop's LDS reads deliver (paired loop: "
+                                         "one read serves a row pair to 64 lanes = 2 chains per "
+                                         "row, half of C*G*P*N*b_obs)"},
                          "hbm": {"algorithmic_gbs": achieved_gbs, "peak": HBM_PEAK_GBS,
                                  "algorithmic_frac": achieved_gbs / HBM_PEAK_GBS,
                                  "measured_gbs": hbm_meas,
@@ -369,8 +525,9 @@ def main():
         }
         print(json.dumps(out))
     eng.close()
-    if pg is not None:
-        pg.destroy_process_group()
+    if hg is not None:
+        hg.barrier()
+        hg.close()
 
 
 if __name__ == "__main__":

@@ -655,20 +655,29 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
   return rc;
 }
 
-// Wait for the context's stream by polling it (hipStreamQuery) for up to 50 ms, then
-// blocking: the blocking wait's wake-up costs ~10 us per call (profiles/r03_launchcost:
-// wall minus event time), a tenth of a 20-iteration run.
+// Wait for the context's stream by polling it (hipStreamQuery), then blocking: the
+// blocking wait's wake-up costs ~10 us per call (profiles/r03_launchcost: wall minus event
+// time), a tenth of a 20-iteration run.  The first 100 us spin; up to 50 ms the poll yields
+// the core between queries (one rank per GPU must not hold a host core each while the CSV
+// writers and init threads need them); after that the blocking wait.  NMC_SYNC_POLL_US sets
+// the polling window (0: block at once).
 int nmc_synchronize(nmc_ctx* x) {
   hipSetDevice(x->device);
+  static const long poll_us = [] {
+    const char* e = getenv("NMC_SYNC_POLL_US");
+    return e ? atol(e) : 50000L;
+  }();
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
-    const hipError_t e = hipStreamQuery(x->stream);
+    const hipError_t e = poll_us > 0 ? hipStreamQuery(x->stream) : hipErrorNotReady;
     if (e == hipSuccess) break;
     if (e != hipErrorNotReady) return fail(-2, std::string("hipStreamQuery: ") + hipGetErrorString(e));
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+    const auto dt = std::chrono::steady_clock::now() - t0;
+    if (dt >= std::chrono::microseconds(poll_us)) {
       HIPCHK(hipStreamSynchronize(x->stream));
       break;
     }
+    if (dt > std::chrono::microseconds(100)) std::this_thread::yield();
   }
   return check_timeout(x);
 }
@@ -930,7 +939,10 @@ int nmc_write_ll_csvs(nmc_ctx* x, const char* dir, const int32_t* chain_ids, int
   const int64_t n_obs = x->n_obs;
   if (rows == 0 || n_obs == 0) return 0;
   if (int rc = ensure_gidx(x)) return rc;
-  const size_t budget = (size_t)256 << 20;
+  // (NMC_LL_BATCH_BYTES: a smaller budget, so the tests can reach the chain-batched branch)
+  size_t budget = (size_t)256 << 20;
+  if (const char* e = getenv("NMC_LL_BATCH_BYTES"))
+    if (atoll(e) > 0) budget = (size_t)atoll(e);
   const size_t per_chain_row = (size_t)n_obs * 8;
   const size_t per_row = (size_t)C * per_chain_row;
   int nb, ncb;   // rows per batch, chains per batch

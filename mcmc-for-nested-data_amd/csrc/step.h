@@ -365,7 +365,7 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
         const int k = gs - lag, kq = k % P, kt = k / P;
         const bool r = nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1));
         if (lane == 0)
-          __hip_atomic_store(lds + L.flag * 64 + 1, r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
+          __hip_atomic_store(lds + L.flag * 64 + 1 + sp, r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (r) {
           // keep the payload loads below the poll (no instruction: wavefront scope)
@@ -459,7 +459,9 @@ nmc_k_step(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int f
 #pragma unroll
       for (int j = 0; j < Fam::NACC; ++j)
         acc[j] = nmc_sum_slots(lds + (L.part + (sp * Fam::NACC + j) * NMC_NSLOT) * 64 + lane);
-      const double verdict = due ? lds[L.flag * 64 + 1] : 0.0;
+      // (one verdict word per step parity, flag words 1-2: the Gibbs wave may already be
+      //  writing step gs+1's verdict while a slow wave reads this one)
+      const double verdict = due ? lds[L.flag * 64 + 1 + sp] : 0.0;
       const double lpc = opk[NMC_OP_LPC * 64], lpp = opk[NMC_OP_LPP * 64];
       const double sA = opk[NMC_OP_SA * 64], sR = opk[NMC_OP_SR * 64];
       const double llp = fam.finish_fast(reg, acc, (long)ngrp, gcst);

@@ -176,11 +176,35 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
     # their likelihoods batched on its own device, concurrently with the others
     if len(devices) > 1:
         with ThreadPoolExecutor(max_workers=len(devices)) as ex:
-            made = list(ex.map(lambda a: make_engine(*a), enumerate(devices)))
+            futs = [ex.submit(make_engine, r, dev) for r, dev in enumerate(devices)]
+        made, err = [], None
+        for f in futs:                 # (every worker has finished: the pool has shut down)
+            try:
+                made.append(f.result())
+            except BaseException as e:   # one device failed: release the others' engines
+                err = err or e
+        if err is not None:
+            for m in made:
+                if m is not None:
+                    m[0].close()
+            raise err
     else:
         made = [make_engine(0, devices[0])]
     engines = [e for e in made if e is not None]
+    try:
+        return _sample_loop(engines, nIter, burn, thin, names, G, partial, saveLogLikelihood,
+                            write_files, sample_dir, threads, displayProgress, return_samples,
+                            logger, chain_logs, start_time)
+    finally:
+        for eng, _, _ in engines:
+            eng.close()
 
+
+def _sample_loop(engines, nIter, burn, thin, names, G, partial, saveLogLikelihood, write_files,
+                 sample_dir, threads, displayProgress, return_samples, logger, chain_logs,
+                 start_time):
+    """The device loop, the per-observation LL rows and the sample files of
+    sample_posterior (the caller closes the engines whatever happens here)."""
     # ---- the device loop ----------------------------------------------------
     rec = record_iterations(nIter, burn, thin)
     if displayProgress:
@@ -216,8 +240,6 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
         if return_samples:
             rows_all.append(numpy.transpose(raw, (2, 0, 1)))
     accept = [eng.accept_counts() for eng, _, _ in engines] if return_samples else None
-    for eng, _, _ in engines:
-        eng.close()
 
     elapsed = datetime.datetime.now() - start_time
     msg = "Finished. The elapsed time in total is %s." \

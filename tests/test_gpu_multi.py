@@ -89,41 +89,53 @@ def test_devices_replay_writes_reference_csvs(gpu_lib, tmp_path, name):
         assert filecmp.cmp(mine, c.csv_path(ch), shallow=False), (name, ch)
 
 
-# ---- two processes (gloo ranks), each driving its own engine on the GPU ----------------
-def _gloo_engine_worker(rank, world, port, q):
+# ---- two processes (host-group ranks), each driving its own engine on the GPU ----------
+def _npy(*arrays):
+    import io
+    f = io.BytesIO()
+    numpy.savez(f, *arrays)
+    return f.getvalue()
+
+
+def _unnpy(blob):
+    import io
+    z = numpy.load(io.BytesIO(blob), allow_pickle=False)
+    return [z["arr_%d" % i] for i in range(len(z.files))]
+
+
+def _host_engine_worker(rank, world, port, q):
     """Rank `rank`: its contiguous shard of the chains (nestmc.parallel.shard), run by an
     engine with chain_base = the shard's first global id; the recorded rows travel to
-    rank 0 over gloo, and bench.py's max-over-ranks timing reduction runs too."""
-    import torch.distributed as dist
+    rank 0 over the product's host group (nestmc.parallel.HostGroup, bench.py's bootstrap),
+    and bench.py's max-over-ranks timing reduction runs too."""
     from nestmc import parallel
     from gpu_cases import partial_state, run_engine, synthetic
     try:
-        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port,
-                                world_size=world, rank=rank)
+        hg = parallel.HostGroup(world, rank, addr="127.0.0.1", port=port, timeout=120)
         C, G, N, n_iter, seed = 70, 5, 30, 24, 19
         fam, sizes, _, _, _ = synthetic("linreg_partial", C, G, N)
         st, _ = partial_state(fam, sizes, C, 2)
         start, count = parallel.shard(C, world, rank)
         sel = numpy.arange(start, start + count)
         acc, _, rows, _ = run_engine(fam, sizes, st, sel, start, n_iter, seed)
-        t = parallel.max_over_ranks(1.0 + rank, dist)
-        out = [None] * world
-        dist.all_gather_object(out, (start, count, acc, rows))
+        t = parallel.max_over_ranks(1.0 + rank, hg)
+        parts = hg.gather(_npy(numpy.array([start, count]), acc, rows))
         if rank == 0:
+            out = [tuple([int(v) for v in a[0]]) + tuple(a[1:]) for a in map(_unnpy, parts)]
             whole = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed)
             q.put(("ok", t, out, whole[0], whole[2]))
-        dist.barrier()
-        dist.destroy_process_group()
+        hg.barrier()
+        hg.close()
     except Exception as e:   # reported to the parent
         q.put(("error", repr(e), None, None, None))
 
 
-def test_two_gloo_ranks_engines_reproduce_one_engine(gpu_lib):
-    """The N > 1 path with the engine on every rank: two processes, one gloo
-    group, each samples its chain shard on the device; the shards are the one-engine run
-    bit for bit (every variate keyed by global chain id)."""
+def test_two_host_ranks_engines_reproduce_one_engine(gpu_lib):
+    """The N > 1 path with the engine on every rank: two processes, one host
+    group (stdlib TCP), each samples its chain shard on the device; the shards are the
+    one-engine run bit for bit (every variate keyed by global chain id)."""
     import socket
-    import torch.multiprocessing as mp
+    import multiprocessing as mp
     world = 2
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -131,7 +143,7 @@ def test_two_gloo_ranks_engines_reproduce_one_engine(gpu_lib):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gloo_engine_worker, args=(r, world, port, q))
+    procs = [ctx.Process(target=_host_engine_worker, args=(r, world, port, q))
              for r in range(world)]
     for p in procs:
         p.start()

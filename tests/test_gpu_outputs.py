@@ -85,3 +85,31 @@ def test_obs_ll_rows_at_final_state_equal_eval_obs_ll(gpu_lib):
     b = eng.eval_obs_ll()
     assert numpy.array_equal(a, b)
     eng.close()
+
+
+def test_ll_csvs_chain_batched_branch_byte_identical(gpu_lib, tmp_path, monkeypatch):
+    """nmc_write_ll_csvs's second branch (one row of every chain over the batch budget:
+    one row of a sub-range of the chains per batch, per-chain 'w' / 'a' opens) writes the
+    one-batch run's files byte for byte.  NMC_LL_BATCH_BYTES shrinks the 256 MiB budget to
+    three chains' rows, so 70 chains take 24 chain blocks x every recorded row."""
+    fam, sizes, priors, pooling, names = synthetic("linreg_partial", 70, 5, 30)
+    value, lp, ll, mu, s2, _ = _state(fam, sizes, 70, 2, pooling)
+    eng = Engine(fam, sizes, 70, pooling, priors, seed=4)
+    eng.set_state(value, lp, ll, mu, s2)
+    eng.set_schedule(50, 20, 3)
+    eng.run(0, 50)
+    eng.synchronize()
+    ids = list(range(7, 77))
+    one, many = tmp_path / "one", tmp_path / "many"
+    one.mkdir()
+    many.mkdir()
+    monkeypatch.delenv("NMC_LL_BATCH_BYTES", raising=False)
+    eng.write_ll_csvs(str(one) + "/", ids, threads=4)
+    monkeypatch.setenv("NMC_LL_BATCH_BYTES", str(3 * int(sum(sizes)) * 8))
+    eng.write_ll_csvs(str(many) + "/", ids, threads=3)
+    monkeypatch.delenv("NMC_LL_BATCH_BYTES")
+    for c in ids:
+        a = (one / ("logLikelihood.%d.csv" % c)).read_bytes()
+        b = (many / ("logLikelihood.%d.csv" % c)).read_bytes()
+        assert a == b and a.count(b"\n") == eng.n_rows, c
+    eng.close()

@@ -49,6 +49,7 @@ def _run_chains(ids):
 
 
 def _worker(rank, port, q):
+    """gloo ranks: the oracle shards gathered over torch.distributed (test harness)."""
     import torch.distributed as dist
     from nestmc import parallel
     try:
@@ -56,13 +57,37 @@ def _worker(rank, port, q):
                                 world_size=WORLD, rank=rank)
         start, count = parallel.shard(C, WORLD, rank)
         rows = _run_chains(range(start, start + count))
-        t = parallel.max_over_ranks(1.0 + rank, dist)
+        t = [None] * WORLD
+        dist.all_gather_object(t, 1.0 + rank)
         out = [None] * WORLD
         dist.all_gather_object(out, (start, count, rows))
         if rank == 0:
-            q.put(("ok", t, out))
+            q.put(("ok", max(t), out))
         dist.barrier()
         dist.destroy_process_group()
+    except Exception as e:   # reported to the parent
+        q.put(("error", repr(e), None))
+
+
+def _host_worker(rank, port, q):
+    """The product's bootstrap (nestmc.parallel.HostGroup, stdlib TCP, no PyTorch): the
+    max-over-ranks timing, the 128-byte id broadcast, barrier and the shards' rows."""
+    import sys
+    from nestmc import parallel
+    try:
+        hg = parallel.HostGroup(WORLD, rank, addr="127.0.0.1", port=port, timeout=60)
+        start, count = parallel.shard(C, WORLD, rank)
+        rows = _run_chains(range(start, start + count))
+        t = parallel.max_over_ranks(1.0 + rank, hg)
+        idb = hg.broadcast(bytes(range(128)) if rank == 0 else None, src=0)
+        hg.barrier()
+        last = hg.broadcast(b"from-1" if rank == 1 else None, src=1)
+        parts = hg.all_gather(numpy.ascontiguousarray(rows).tobytes())
+        if rank == 0:
+            q.put(("ok", (t, idb, last, [len(p) for p in parts], "torch" in sys.modules),
+                   (start, count, parts)))
+        hg.barrier()
+        hg.close()
     except Exception as e:   # reported to the parent
         q.put(("error", repr(e), None))
 
@@ -109,3 +134,26 @@ def test_padded_shards_and_assembly():
     # balanced split covers every chain once
     parts = [parallel.shard(13, 3, r) for r in range(3)]
     assert sum(c for _, c in parts) == 13 and parts[0] == (0, 5) and parts[2] == (9, 4)
+
+
+def test_host_group_bootstrap_two_processes():
+    """nestmc.parallel.HostGroup (what bench.py and the RCCL bootstrap use): two spawned
+    processes, no PyTorch imported, the shard rows merged on rank 0 equal one run."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    status, info, payload = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    assert status == "ok", info
+    t, idb, last, sizes, torch_loaded = info
+    assert t == float(WORLD) and idb == bytes(range(128)) and last == b"from-1"
+    assert not torch_loaded                         # the bootstrap needs no PyTorch
+    whole = _run_chains(range(C))
+    got = [numpy.frombuffer(b, dtype=numpy.float64) for b in payload[2]]
+    assert numpy.array_equal(numpy.concatenate(got), numpy.concatenate(
+        [whole[:4].ravel(), whole[4:].ravel()]))
