@@ -323,12 +323,13 @@ def measure_traffic(args):
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
+                        kn = row.get("Kernel_Name", "")
                         if row.get("Counter_Name") == counter and \
-                                "nmc_k_run" in row.get("Kernel_Name", ""):
+                                ("nmc_k_run" in kn or "nmc_k_sweep" in kn):
                             rows.append((int(row.get("Dispatch_Id", 0)),
                                          float(row["Counter_Value"])))
             if len(rows) < 2:
-                return {"error": "no %s rows for nmc_k_run" % counter}
+                return {"error": "no %s rows for the step kernel" % counter}
             out[counter] = sorted(rows)[-1][1]       # the K-iteration launch (the last)
     finally:
         shutil.rmtree(base, ignore_errors=True)

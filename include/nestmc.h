@@ -211,6 +211,10 @@ int nmc_debug_igamci(const double* a, const double* q, const double* lga, int n,
                      double* out);
 int nmc_debug_rng(const uint32_t* ctr5, int n, uint32_t seed, double gamma_shape,
                   double* out4);
+/* numpy.logaddexp(0, x[i]) as the likelihood kernels evaluate it (csrc/softplus.h): on the
+ * host (on_device = 0, no GPU needed) or by a device kernel (on_device = 1); the two are
+ * bit-identical by construction (IEEE add / mul / fma / div, rint, ldexp only).          */
+int nmc_debug_softplus(const double* x, int n, double* out, int on_device);
 /* Diagnostic build only (make stamps -> libnestmc_stamps.so): shader-clock phase
  * stamps of the step kernel, [2 blocks][2 waves][8 iterations][16 slots]; n > 0
  * arms (zeroes) the buffer, out != NULL copies it back.  Error in the shipped lib. */

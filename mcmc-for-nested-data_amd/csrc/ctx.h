@@ -16,6 +16,7 @@
 #include "../../include/nestmc.h"
 #include "kernels.h"
 #include "step.h"
+#include "sweep.h"
 
 // error message of the calling thread (nestmc.hip); returns code
 int nmc_fail(int code, const std::string& msg);
@@ -60,6 +61,8 @@ struct nmc_ctx {
   void* user = nullptr;                   // user family: its per-device kernel table (user.hip)
   double* user_k = nullptr;               // user family: device copy of the model constants
   bool step_ok = false;                   // nmc_k_step where it applies (NMC_STEP=1)
+  bool sweep = false;                     // nmc_k_sweep runs the loop (choose_geometry)
+  bool no_sweep = false;                  // (its grid could not be resident: nmc_k_run)
 };
 
 static inline double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->d.vb0; }
@@ -75,6 +78,7 @@ static inline size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
 }
 static inline int run_mode(const nmc_ctx* x) {
   if (x->pooling != NMC_POOL_PARTIAL) return x->d.CL == 32 ? NMC_MODE_HALF : NMC_MODE_NOPOOL;
+  if (x->sweep) return x->d.G <= 64 ? NMC_MODE_SYNC_REG : NMC_MODE_SYNC_LDS;
   if (!x->persistent) return NMC_MODE_LAUNCH;
   if (x->d.hreg) return x->d.hown ? NMC_MODE_SYNC_OWN : NMC_MODE_SYNC_REG;
   return x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
@@ -93,7 +97,14 @@ static inline size_t step_lds_bytes(const nmc_ctx* x) {
                               x->d.nmax * x->nf, x->d.G).total * 512;
 }
 
+// LDS of nmc_k_sweep (sweep.h)
+static inline size_t sweep_lds_bytes(const nmc_ctx* x) {
+  return (size_t)nmc_sweep_lds(x->nacc, x->d.P, x->pooling == NMC_POOL_PARTIAL,
+                               x->d.G > 64 ? 1 : 0, x->d.G, x->d.nmax * x->nf).total * 512;
+}
+
 static inline size_t run_lds_bytes(const nmc_ctx* x) {
+  if (x->sweep) return sweep_lds_bytes(x);
   if (uses_step(x, run_mode(x))) return step_lds_bytes(x);
   return lds_bytes_for(x, x->persistent && x->d.hlds ? 1 : 0, x->d.rows_lds);
 }
@@ -109,11 +120,13 @@ static inline int nmc_safe_blocks(const nmc_ctx* x, int nb) {
 }
 // mode of the persistent partial-pooling kernel (its occupancy query)
 static inline int nmc_persist_mode(const nmc_ctx* x) {
+  if (x->sweep) return run_mode(x);
   return x->d.hreg ? (x->d.hown ? NMC_MODE_SYNC_OWN : NMC_MODE_SYNC_REG)
                    : x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
 }
 // LDS of the persistent partial-pooling kernel (its occupancy query)
 static inline size_t nmc_persist_lds(const nmc_ctx* x) {
+  if (x->sweep) return sweep_lds_bytes(x);
   if (uses_step(x, nmc_persist_mode(x))) return step_lds_bytes(x);
   return lds_bytes_for(x, x->d.hlds && !x->d.hreg, x->d.rows_lds);
 }
@@ -196,7 +209,20 @@ int nmc_call_logistic(nmc_ctx* x, NmcCall& c);
 int nmc_call_user(nmc_ctx* x, NmcCall& c);
 int nmc_user_attach(nmc_ctx* x, int family);   // load the module on x's device, check shapes
 
+// the sweep kernel's launches and occupancy queries (sweep_*.hip)
+int nmc_sweep_linreg(nmc_ctx* x, NmcCall& c);
+int nmc_sweep_gauss_mean(nmc_ctx* x, NmcCall& c);
+int nmc_sweep_logistic(nmc_ctx* x, NmcCall& c);
+
 static inline int nmc_call_family(nmc_ctx* x, NmcCall& c) {
+  if (x->sweep && x->family < NMC_LL_USER_BASE &&
+      (c.op == NMC_OP_RUN || c.op == NMC_OP_CAN_PERSIST || c.op == NMC_OP_CAPACITY)) {
+    switch (x->family) {
+      case NMC_LL_LINREG: return nmc_sweep_linreg(x, c);
+      case NMC_LL_GAUSS_MEAN: return nmc_sweep_gauss_mean(x, c);
+      case NMC_LL_LOGISTIC: return nmc_sweep_logistic(x, c);
+    }
+  }
   switch (x->family) {
     case NMC_LL_LINREG: return nmc_call_linreg(x, c);
     case NMC_LL_GAUSS_MEAN: return nmc_call_gauss_mean(x, c);

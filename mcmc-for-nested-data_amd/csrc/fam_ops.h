@@ -109,6 +109,14 @@ static int nmc_fam_call(nmc_ctx* x, const Fam& fam, NmcCall& c) {
 }
 
 // nmc_call_<family>: (n_fields) -> the concrete functor type, then the op.
+// (NMC_ONLY_NF=k, register-budget experiments only: instantiate one row width)
+#ifdef NMC_ONLY_NF
+#define NMC_DEFINE_FAMILY_CALL(NAME, MAKE)                                  \
+  int NAME(nmc_ctx* x, NmcCall& c) {                                        \
+    if (x->nf == NMC_ONLY_NF) return nmc_fam_call(x, MAKE<NMC_ONLY_NF>(x->llc), c); \
+    return nmc_fail(-1, "NMC_ONLY_NF build");                               \
+  }
+#else
 #define NMC_DEFINE_FAMILY_CALL(NAME, MAKE)                                  \
   int NAME(nmc_ctx* x, NmcCall& c) {                                        \
     switch (x->nf) {                                                        \
@@ -124,3 +132,4 @@ static int nmc_fam_call(nmc_ctx* x, const Fam& fam, NmcCall& c) {
     }                                                                       \
     return nmc_fail(-1, "n_fields must be 1..9");                           \
   }
+#endif

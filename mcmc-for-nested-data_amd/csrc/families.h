@@ -21,18 +21,15 @@
 #endif
 
 #include "special.h"
+#include "softplus.h"
 
 #define NMC_MAXP 16
 
 // numpy.logaddexp(0, eta) (npy_logaddexp: x == y -> x + ln 2; else max + log1p(exp(-|x - y|)),
-// NaN propagating), branch-free: one exp and one log1p per lane whatever the sign of eta, so
-// lanes whose eta differ in sign do not run both halves.  Bit-identical to the branchy form:
-// eta < 0 gives 0.0 + log1p(exp(eta)) == log1p(exp(eta)); +-inf give inf / 0; NaN gives NaN.
-__device__ __forceinline__ double nmc_logaddexp0(double eta) {
-  const double m = eta > 0.0 ? eta : 0.0;
-  const double r = m + log1p(exp(-fabs(eta)));
-  return eta == 0.0 ? NMC_LN2 : r;
-}
+// NaN propagating), branch-free: one range-reduced exp and one range-reduced log1p per lane
+// whatever the sign of eta (softplus.h: ~50 VALU instructions against 181 for the library's
+// exp + log1p, within 2.5 ulp).  +-inf give inf / 0, NaN gives NaN, eta == 0 gives ln 2.
+__device__ __forceinline__ double nmc_logaddexp0(double eta) { return nmc_softplus(eta); }
 
 // ---------------------------------------------------------------------------
 // Gaussian linear regression (example/regression.py:53-67; cfg 3/4 with sigma=1):

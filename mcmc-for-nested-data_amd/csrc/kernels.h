@@ -1532,9 +1532,24 @@ enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
 // RL: the groups' rows are staged in LDS for the launch (d.rows_lds) -- a template
 // parameter so each instance holds only its own row loop (the LDS-DMA staged loop's
 // registers raised the rows-in-LDS kernel's pressure: ~5 % of its time at cfg 3)
+// The step kernel's Dev argument (the first kernel argument: offset 0 of the kernarg
+// segment) read through a pointer laundered at the top of every step: its fields are
+// scalar-loaded (s_load, scalar cache) where a step uses them instead of being hoisted out
+// of the persistent loop and held in SGPRs for the whole launch -- some 60 fields, which
+// spilled 160-600 SGPRs per instance (MI355X: <= 102 SGPRs per wave).
+typedef __attribute__((address_space(4))) const Dev* nmc_kdev_ptr;
+__device__ __forceinline__ const Dev* nmc_kdev() {
+  nmc_kdev_ptr p = (nmc_kdev_ptr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return (const Dev*)p;
+}
+
 template <class Fam, int MODE, bool RL = true>
 __global__ void __launch_bounds__(NMC_RUN_THREADS)
-nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int flags) {
+nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, int flags) {
+  (void)d_arg;   // (read through nmc_kdev(): the same bytes)
+  const Dev* dP = nmc_kdev();
+#define d (*dP)
   constexpr bool PARTIAL = MODE != NMC_MODE_NOPOOL && MODE != NMC_MODE_HALF;
   // half layout: the grid of 64-chain blocks would leave CUs idle (none/complete pooling,
   // RB * G * 2 <= CUs): 32 chains per workgroup, twice the workgroups, each lane pair
@@ -1798,6 +1813,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     };
     for (int t = i0; t < i1 && ok; ++t) {
       for (int p = 0; p < P; ++p) {
+        dP = nmc_kdev();
         const int gs = t * P + p;
         const bool due = gs - lag >= gs0;
         bool okw = P == 1 ? owner_task(gs - 1) : true;
@@ -1882,6 +1898,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     const int gs0 = i0 * P;
     for (int t = i0; t < i1 && ok; ++t) {
       for (int p = 0; p < P; ++p) {
+        dP = nmc_kdev();
         const int gs = t * P + p;
         const bool due = gs - lag >= gs0;
         gibbs_step(t, p);
@@ -1912,6 +1929,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
     NMC_STAMP(t, 0);
     const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
     for (int p = 0; p < P; ++p) {
+      dP = nmc_kdev();
       const int sp = (t * P + p) & 1;
       double c_prop, c_v, c_lu, c_lpc, c_lpp, c_sA, c_sR;   // control wave, this step
       // the proposal's prepared parameters, formed before barrier A (the other values
@@ -2232,6 +2250,7 @@ nmc_k_run(Dev d, Fam fam, const double* __restrict__ obs, int i0, int i1, int fl
       nmc_hyper<NMC_SRC_SC1>(d, ((i1 - 1) & 1) ? d.vb1 : d.vb0, cb, i1 - 1, lds, L, true);
   }
   NMC_RUN_SL(3);
+#undef d
 }
 
 // Group log-likelihoods for arbitrary theta [P][G][C] (the batched start-point search and

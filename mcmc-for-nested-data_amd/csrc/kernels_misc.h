@@ -102,3 +102,8 @@ __global__ void nmc_k_debug_rng(const uint32_t* ctr, int n, uint32_t seed, doubl
   out[4 * i + 2] = u.b;
   out[4 * i + 3] = nmc_gamma_mt(ga, k[0], k[2], k[4], seed);
 }
+
+__global__ void nmc_k_debug_softplus(const double* x, int n, double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = nmc_softplus(x[i]);
+}

@@ -138,6 +138,27 @@ static void choose_geometry(nmc_ctx* x) {
     d.CL = 32;
     d.RB = (d.C + d.CL - 1) / d.CL;
   }
+
+  // nmc_k_sweep (sweep.h): rows in LDS, no row split, none/complete pooling or partial
+  // pooling over one numpy leaf (G <= 128); up to 12 waves per workgroup (three per SIMD,
+  // <= 168 VGPRs), fewer when the grid needs two or three workgroups per CU.  Bit-identical
+  // to nmc_k_run; NMC_SWEEP=0 keeps nmc_k_run (the tests compare them).
+  x->sweep = false;
+  if (d.rows_lds && d.S == 1 && !x->step_ok && !x->no_sweep &&
+      !(getenv("NMC_SWEEP") && !atoi(getenv("NMC_SWEEP"))) &&
+      (x->pooling != NMC_POOL_PARTIAL || (d.G <= 128 && d.nleaf == 1))) {
+    const int64_t wgs = (int64_t)d.RB * d.G;
+    int sw = wgs <= x->ncu ? NMC_SWEEP_THREADS / 64 : wgs <= 2 * (int64_t)x->ncu ? 6 : 4;
+    if (const char* e = getenv("NMC_SWEEP_WAVES")) {
+      const int v = atoi(e);
+      if (v >= 3 && v <= NMC_SWEEP_THREADS / 64) sw = v;
+    }
+    // partial pooling: a control, a Gibbs and at least one likelihood wave, all resident
+    if (x->pooling != NMC_POOL_PARTIAL || wgs <= 3 * (int64_t)x->ncu) {
+      x->sweep = true;
+      d.W = sw;
+    }
+  }
 }
 
 // numpy's pairwise-sum recursion over G groups (numpy/_core/src/umath/loops_utils.h):
@@ -378,6 +399,11 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     NmcCall c;
     c.op = NMC_OP_CAN_PERSIST;
     if (int rc2 = nmc_call_family(x, c)) { nmc_destroy(x); return rc2; }
+    if (x->sweep && c.result != 1) {   // the sweep grid cannot be resident: nmc_k_run
+      x->no_sweep = true;
+      choose_geometry(x);
+      if (int rc2 = nmc_call_family(x, c)) { nmc_destroy(x); return rc2; }
+    }
     // row split: always persistent (the members exchange every step), in resident batches
     // of chain blocks when the whole grid is not (chain blocks are independent)
     x->persistent = c.result == 1 || d.S > 1;
@@ -618,7 +644,10 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       // every variate of iterations [c0, c1) in one fully parallel launch: the hyper
       // variates (partial pooling) and the step variates (unless the step kernel draws them)
       x->d.vbase = c0;
-      const size_t n = (size_t)(c1 - c0) * P * x->C * ((x->d.zin ? 0 : x->G) + (partial ? 1 : 0));
+      // (nmc_k_sweep draws every variate itself)
+      const size_t n = x->sweep ? 0
+                                : (size_t)(c1 - c0) * P * x->C *
+                                      ((x->d.zin ? 0 : x->G) + (partial ? 1 : 0));
       if (n) {
         const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);
         hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);
@@ -822,6 +851,11 @@ int nmc_kernel_name(nmc_ctx* x, char* out, int cap) {
     case NMC_LL_GAUSS_MEAN: fam = "FamGaussMean<" + std::to_string(x->nf) + ">"; break;
     case NMC_LL_LOGISTIC: fam = "FamLogistic<" + std::to_string(x->nf) + ">"; break;
     default: fam = "FamUser"; break;
+  }
+  if (x->sweep) {
+    snprintf(out, (size_t)(cap > 0 ? cap : 1), "%s",
+             ("nmc_k_sweep<" + fam + ", " + modes[mode] + ">").c_str());
+    return cap < 1 ? fail(-1, "kernel name: cap < 1") : 0;
   }
   std::string k = uses_step(x, mode)
                       ? "nmc_k_step<" + fam + ", " + modes[mode] + ">"
@@ -1180,6 +1214,25 @@ int nmc_debug_rng(const uint32_t* ctr5, int n, uint32_t seed, double gamma_shape
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(out4, dout, (size_t)n * 4 * 8, hipMemcpyDeviceToHost));
   hipFree(dc); hipFree(dout);
+  return 0;
+}
+
+int nmc_debug_softplus(const double* x, int n, double* out, int on_device) {
+  if (n < 0) return fail(-1, "n < 0");
+  if (!on_device) {
+    for (int i = 0; i < n; ++i) out[i] = nmc_softplus(x[i]);
+    return 0;
+  }
+  double *dx, *dout;
+  HIPCHK(hipMalloc(&dx, (size_t)(n ? n : 1) * 8));
+  HIPCHK(hipMalloc(&dout, (size_t)(n ? n : 1) * 8));
+  HIPCHK(hipMemcpy(dx, x, (size_t)n * 8, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(nmc_k_debug_softplus, dim3((n + 255) / 256 > 0 ? (n + 255) / 256 : 1),
+                     dim3(256), 0, 0, (const double*)dx, n, dout);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost));
+  hipFree(dx);
+  hipFree(dout);
   return 0;
 }
 

@@ -1,0 +1,582 @@
+// sweep.h -- nmc_k_sweep<Fam, MODE>: the step kernel for groups whose rows fit LDS and need
+// no row split, in three waves per SIMD.
+//
+// Same work, tile partition, summation orders, variates and outputs as nmc_k_run
+// (kernels.h) -- the two are bit-identical and the tests compare them -- built around what
+// MI355X measurements say bounds the loop (profiles/r04_fp64issue.jsonl): one wave issues an
+// fp64 VALU instruction at most every ~5.8 cycles, two waves on a SIMD every ~4.7, three
+// every ~4.5 (the paired row loop with its LDS reads: 7.0 / 5.3 / 4.9).  nmc_k_run's eight
+// waves leave the SIMDs of its control and Gibbs waves with one likelihood wave for most
+// of a step; here 12 waves (768 threads, <= 168 VGPRs) keep two or three likelihood waves
+// on every SIMD while the roles run.  The kernel holds few values across its persistent
+// loop: Dev is read through a pointer laundered at the top of every step (nmc_kdev), and
+// each role's values live in its own branch (the Gibbs wave's 64-value payload never shares
+// registers with the row loop).  Every variate is drawn inside the kernel, so no fill
+// kernel runs before it:
+//   * {z, log u} of step (t, p) (Parameter.propose :304-306, the accept uniform :362):
+//     entry 0 of the previous step's tile queue (nmc_step_variate, the fill's function);
+//   * {hyper z, Gamma((G-1)/2)} of a Gibbs task (HyperParameter.update :481-498): drawn by
+//     the Gibbs wave for its own task (nmc_hyper_variate, the fill's function).
+//
+// MODE (kernels.h NMC_MODE_*):
+//   NOPOOL    none / complete pooling, 64 chains per workgroup
+//   HALF      none / complete pooling, 32 chains per workgroup (lanes l, l + 32: one chain)
+//   SYNC_REG  partial pooling, G <= 64: the Gibbs wave fetches a task's G published values
+//             into registers (one sc1 round trip) -- nmc_k_run's register hand-off
+//   SYNC_LDS  partial pooling, 64 < G <= 128 (one numpy leaf): the same hand-off with the
+//             payload moved to LDS by LDS-DMA, updated from there (nmc_hyper_compute)
+// Wave roles per step k = (t, p):
+//   wave 0   control: the deferred state update of step k-1, the decision's operands (both
+//            counter outcomes, tuned scales, priors), the count of the last published value;
+//            then likelihood tiles; after barrier A the slot sum, finish and the Metropolis
+//            decision (:334-383), published write-through (partial pooling)
+//   wave 1   (partial) Gibbs: task k - lag (poll, fetch, pairwise update, this step's priors
+//            when they need it), then barrier A / B with the others
+//   others   likelihood tiles from the step's LDS queue (entry 0: the next step's variates)
+#pragma once
+#include "kernels.h"
+
+#ifndef NMC_SWEEP_THREADS
+#define NMC_SWEEP_THREADS 768
+#endif
+
+// LDS carve of nmc_k_sweep, in columns of 64 doubles (one per lane); the host computes the
+// same (ctx.h).
+struct nmc_sweep_layout {
+  int th;     // [P]            current values
+  int part;   // [NACC][NSLOT]  tile partial sums (unused slots: -0.0)
+  int st;     // [5][P]         scale, log prior, n acc, n rej, total acc (NMC_ST_*)
+  int hyp;    // [6][P]         hyper state (NMC_HY_*), partial pooling
+  int hval;   // [G + 1]        SYNC_LDS: the Gibbs payload (+1: the DMA moves group pairs)
+  int zl;     // [2][2]         {z, log u} of this and the next step (step parity)
+  int cw;     // [8]            control values across the barriers (NMC_CW_*)
+  int flag;   // [1]            word 0 wait flag, words 1-2 Gibbs verdict by step parity,
+              //                uint32 words 8-9 the tile queues by step parity
+  int rows;   // [nrows][NF]    the group's rows, staged once per launch
+  int total;  // columns
+};
+__host__ __device__ inline nmc_sweep_layout nmc_sweep_lds(int nacc, int P, int partial,
+                                                          int hlds, int G, int row_doubles) {
+  nmc_sweep_layout L;
+  L.th = 0;
+  L.part = L.th + P;
+  L.st = L.part + nacc * NMC_NSLOT;
+  L.hyp = L.st + 5 * P;
+  L.hval = L.hyp + (partial ? 6 * P : 0);
+  L.zl = L.hval + (partial && hlds ? G + 1 : 0);
+  L.cw = L.zl + 4;
+  L.flag = L.cw + 8;
+  L.rows = L.flag + 1;
+  // (+1 column: the pipelined likelihood loop prefetches one block past a wave's rows)
+  L.total = L.rows + (row_doubles > 0 ? (row_doubles + 63) / 64 + 1 : 0);
+  return L;
+}
+
+// Out-of-line helpers: the variate draws and the none/complete-pooling priors run once per
+// step on one wave; kept out of the step loop's body so their many polynomial constants are
+// materialized where they are used rather than hoisted into registers for the whole launch.
+// {z, log u} of step (it, p) of group g, chain c (nmc_step_variate: nmc_k_fill's values).
+__device__ __noinline__ nmc_d2 nmc_sweep_step_variate(const double* rz, const double* ru,
+                                                      int replay_n, int rng_mode, int P, int G,
+                                                      int C, uint32_t ch, uint32_t seed, int it,
+                                                      int p, int g, int c) {
+  nmc_d2 r;
+  if (rng_mode == NMC_RNG_MODE_REPLAY) {
+    const size_t k = (((size_t)it * P + p) * G + g) * C + c;
+    r.a = it < replay_n ? rz[k] : nmc_nan();
+    r.b = it < replay_n ? log(ru[k]) : nmc_nan();
+  } else {
+    r.a = nmc_normal(it, g, p, NMC_PURPOSE_PROPOSAL, ch, seed);
+    r.b = log(nmc_uniform2(it, g, p, NMC_PURPOSE_ACCEPT, ch, seed).a);
+  }
+  return r;
+}
+// {hyper z, Gamma(a) draw} of the Gibbs update of parameter q after iteration t for chain c
+// (nmc_k_fill's values: Philox normal and Marsaglia-Tsang, or the replayed reference draws
+// through scipy's inverse-CDF path).
+__device__ __noinline__ nmc_d2 nmc_sweep_hyper_variate(const double* rhz, const double* rhu,
+                                                       int replay_n, int rng_mode, int P, int C,
+                                                       uint32_t ch, uint32_t seed, double ha,
+                                                       double hlga, int t, int q, int c) {
+  nmc_d2 r;
+  if (rng_mode == NMC_RNG_MODE_REPLAY) {
+    const size_t k = ((size_t)t * P + q) * C + c;
+    r.a = t < replay_n ? rhz[k] : nmc_nan();
+    r.b = t < replay_n ? nmc_igamci(ha, rhu[k], hlga) : nmc_nan();
+  } else {
+    r.a = nmc_normal(t, 0, q, NMC_PURPOSE_HYPER_NORMAL, ch, seed);
+    r.b = nmc_gamma_mt(ha, t, q, ch, seed);
+  }
+  return r;
+}
+__device__ __noinline__ double nmc_sweep_prior(int fam, const double* prm, double x) {
+  return nmc_prior_logpdf(fam, prm, x);
+}
+
+// The kernel's only argument (one struct, so the kernarg segment holds it at offset 0 and
+// every field is read through the laundered pointer of nmc_sweep_args_at).
+template <class Fam>
+struct nmc_sweep_args {
+  Dev d;
+  Fam fam;
+  int i0, i1;
+};
+template <class Fam>
+__device__ __forceinline__ const nmc_sweep_args<Fam>* nmc_sweep_args_at() {
+  typedef __attribute__((address_space(4))) const nmc_sweep_args<Fam>* kp;
+  kp q = (kp)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(q));
+  return (const nmc_sweep_args<Fam>*)q;
+}
+
+template <class Fam, int MODE>
+__global__ void __launch_bounds__(NMC_SWEEP_THREADS)
+nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
+  (void)a_arg;   // (read through nmc_sweep_args_at(): the same bytes)
+  constexpr bool PARTIAL = MODE == NMC_MODE_SYNC_REG || MODE == NMC_MODE_SYNC_LDS;
+  constexpr bool HREG = MODE == NMC_MODE_SYNC_REG;
+  constexpr bool HALF = MODE == NMC_MODE_HALF;
+  constexpr int NF = Fam::NFIELDS;
+  constexpr int MP = Fam::MAXP;
+  static_assert(MODE == NMC_MODE_NOPOOL || MODE == NMC_MODE_HALF || PARTIAL, "sweep modes");
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const nmc_sweep_args<Fam>* A = nmc_sweep_args_at<Fam>();
+#define d (A->d)
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int W = blockDim.x >> 6;
+  const int i0 = A->i0, i1 = A->i1;
+  const int g = blockIdx.x % d.G, cb = blockIdx.x / d.G;
+  const int c = HALF ? cb * 32 + (lane & 31) : cb * 64 + lane;
+  const bool live = c < d.C && (!HALF || lane < 32);   // writes this lane's outputs
+  const int cc = c < d.C ? c : d.C - 1;
+  const bool ctl = w == 0;
+  const bool gw = PARTIAL && w == 1;                    // the Gibbs wave
+  const bool g0w = g == 0;                              // writes the chain block's hyper state
+  // Everything else is re-derived from the laundered arguments where a step needs it, so the
+  // persistent loop holds few values in registers: the step's view of the problem.
+  struct View {
+    int P, G, C, lag, gs0, ge, ngrp;
+    size_t gc;
+    nmc_sweep_layout L;
+    nmc_tiling TI;
+  };
+  auto view = [&]() {
+    View v;
+    v.P = d.P; v.G = d.G; v.C = d.C;
+    v.lag = v.P >= 2 ? 2 : 1;                           // Gibbs task of step gs: gs - lag
+    v.gs0 = i0 * v.P; v.ge = i1 * v.P;
+    v.ngrp = (int)(d.off[g + 1] - d.off[g]);
+    v.gc = (size_t)g * v.C + cc;
+    v.L = nmc_sweep_lds(Fam::NACC, v.P, PARTIAL, MODE == NMC_MODE_SYNC_LDS, v.G, d.nmax * NF);
+    v.TI = nmc_tiles(v.ngrp, d.tile);
+    return v;
+  };
+  auto hl_view = [](const nmc_sweep_layout& L) {   // the Gibbs helpers' view of the carve
+    nmc_lds_layout H;
+    H.hval = L.hval;
+    H.hyp = L.hyp;
+    H.flag = L.flag;
+    return H;
+  };
+  // the task this workgroup closes after the loop: ge-lag+g (groups 0 .. lag-1), -1: none
+  auto close_task = [&](const View& v) {
+    const int k0 = v.ge - v.lag > v.gs0 ? v.ge - v.lag : v.gs0;
+    return PARTIAL && k0 + g < v.ge ? k0 + g : -1;
+  };
+  // {z, log u} of step (tn, pn) -> LDS slot `slot` (this lane's chain)
+  auto put_variates = [&](const View& v, int tn, int pn, int slot) {
+    const nmc_d2 r = nmc_sweep_step_variate(d.rz, d.ru, d.replay_n, d.rng_mode, v.P, v.G, v.C,
+                                            (uint32_t)(d.chain_base + cc), d.seed, tn, pn, g, cc);
+    lds[(v.L.zl + 2 * slot) * 64 + 2 * lane] = r.a;
+    lds[(v.L.zl + 2 * slot) * 64 + 2 * lane + 1] = r.b;
+  };
+
+  NMC_RUN_SL(0);
+  // ---- prologue: the group's rows -> LDS (LDS-DMA, 1 KiB per wave-instruction), values and
+  //      state -> LDS (parameter p by wave p % W) ----
+  {
+    const View v = view();
+    const nmc_sweep_layout& L = v.L;
+    double* lrows = lds + L.rows * 64;
+    const int64_t ra0 = d.off[g];
+    const double* grows = d.obs + ra0 * NF;
+    const int nd = v.ngrp * NF;
+    if (((ra0 * NF) & 1) == 0) {   // 16-byte pieces; an odd nd copies one double of slack
+      const int npc = (nd + 1) / 2;
+      for (int b0 = w * 64; b0 < npc; b0 += W * 64)
+        if (b0 + lane < npc) nmc_dma16(grows + 2 * (b0 + lane), lrows + 2 * b0);
+    } else {
+      for (int i = threadIdx.x; i < nd; i += blockDim.x) lrows[i] = grows[i];
+    }
+    const int P = v.P, G = v.G, C = v.C;
+    double* th = lds + L.th * 64 + lane;
+    double* st = lds + L.st * 64 + lane;
+    double* hy = lds + L.hyp * 64 + lane;
+    const double* vin = ((i0 - 1) & 1) ? d.vb1 : d.vb0;
+    for (int p = w; p < P; p += W) {
+      const size_t ip = (size_t)p * G * C + v.gc;
+      th[p * 64] = vin[ip];
+      st[(NMC_ST_S * P + p) * 64] = d.scale[ip];
+      st[(NMC_ST_LP * P + p) * 64] = d.lp[ip];
+      st[(NMC_ST_NA * P + p) * 64] = (double)d.nacc[ip];
+      st[(NMC_ST_NR * P + p) * 64] = (double)d.nrej[ip];
+      st[(NMC_ST_TA * P + p) * 64] = (double)d.tacc[ip];
+      if (PARTIAL) {   // hyper-parameters after iteration i0-1 (slot (i0-1) & 1)
+        const size_t ho = nmc_hslot(d, i0 - 1) + (size_t)p * C + cc;
+        const double s2 = d.s2[ho];
+        hy[(NMC_HY_MU * P + p) * 64] = d.mu[ho];
+        hy[(NMC_HY_SD * P + p) * 64] = d.hsd[ho];
+        hy[(NMC_HY_LSD * P + p) * 64] = d.hlsd[ho];
+        hy[(NMC_HY_S2 * P + p) * 64] = s2;
+        hy[(NMC_HY_SDM * P + p) * 64] = sqrt(s2 / G);
+        hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / d.hsd[ho];
+      }
+    }
+    if (ctl) {
+      put_variates(v, i0, 0, v.gs0 & 1);   // {z, log u} of the launch's first step
+      for (int j = 0; j < Fam::NACC; ++j)   // x + (-0.0) == x: the fixed slot sum
+        for (int k = v.TI.nt; k < NMC_NSLOT; ++k)
+          lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = -0.0;
+      lds[L.flag * 64 + lane] = 0.0;       // (also zeroes the tile queues)
+    }
+    nmc_drain_vm();                        // this wave's row DMA has landed
+  }
+  __syncthreads();
+  NMC_RUN_SL(1);
+
+  bool ok = true;
+  // ---- the Gibbs wave: its own loop, meeting the others at both barriers of every step ----
+  if constexpr (PARTIAL) if (gw) {
+    if (!(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
+    // task k = (kt, kq): poll its publication, update (HyperParameter.update :463-498),
+    // write (the global slot of kt and the sample row); priors: this step's priors from the
+    // update (p, sp, t: the step); returns the poll's verdict
+    auto task = [&](const View& v, int k, bool write, bool priors, int p, int sp, int t) -> bool {
+      const int P = v.P, G = v.G, C = v.C;
+      const nmc_sweep_layout& L = v.L;
+      const int kq = k % P, kt = k / P;
+      const bool r = nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1));
+      if (!r) return false;
+      // keep the payload loads below the poll (no instruction: wavefront scope)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const nmc_d2 hv = nmc_sweep_hyper_variate(d.rhz, d.rhu, d.replay_n, d.rng_mode, P, C,
+                                                (uint32_t)(d.chain_base + cc), d.seed, d.ha,
+                                                d.hlga, kt, kq, cc);
+      if constexpr (HREG) {
+        double xv[64];
+        const double* src = ((kt & 1) ? d.vb1 : d.vb0) + (size_t)kq * G * C + cc;
+#pragma unroll
+        for (int u = 0; u < 64; ++u) xv[u] = nmc_ldv<NMC_SRC_SC1>(src + (size_t)u * C);
+        nmc_hyper_compute_reg(d, cb, kt, kq, lds, L.hyp, write, hv.a, hv.b, xv);
+      } else {
+        const nmc_lds_layout H = hl_view(L);
+        const double* src = (kt & 1) ? d.vb1 : d.vb0;
+        if ((C & 1) == 0) {
+          nmc_hyper_dma(d, src, kq, cb, 0, G, lds, H, 0);
+          nmc_drain_vm();
+        } else {
+          nmc_hyper_load(d, src, kq, cc, 0, G, lds, H, 0);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        nmc_hyper_compute(d, cb, kt, kq, lds, H, write, hv.a, hv.b, 0);
+      }
+      if (priors) {   // the update lands in the step that needs it: this step's priors
+        const double* th = lds + L.th * 64 + lane;
+        const double* st = lds + L.st * 64 + lane;
+        const double* hy = lds + L.hyp * 64 + lane;
+        double* cwv = lds + L.cw * 64 + lane;
+        const double x = th[p * 64];
+        const double prop = x + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
+                                    lds[(L.zl + 2 * sp) * 64 + 2 * lane];
+        const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
+        const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
+        cwv[NMC_CW_LPC * 64] =
+            t > 0 ? nmc_norm_logpdf_r(x, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
+        cwv[NMC_CW_LPP * 64] = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
+      }
+      return true;
+    };
+    for (int t = i0; t < i1 && ok; ++t) {
+      for (int p = 0; p < d.P; ++p) {
+        A = nmc_sweep_args_at<Fam>();
+        const View v = view();
+        const int gs = t * v.P + p, sp = gs & 1;
+        const bool due = gs - v.lag >= v.gs0;
+        if (due) {
+          const bool r = task(v, gs - v.lag, g0w, v.P <= 2, p, sp, t);
+          if (lane == 0)
+            __hip_atomic_store(lds + v.L.flag * 64 + 1 + sp,
+                               r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();   // A
+        if (due) {
+          ok = lds[v.L.flag * 64 + 1 + sp] == 2.0 * ((double)gs + 1);
+          if (!ok) break;
+        }
+        __syncthreads();   // B
+      }
+    }
+    // closing: task close_k (the matching barrier of the other waves' nmc_wait_published)
+    A = nmc_sweep_args_at<Fam>();
+    const View v = view();
+    const int close_k = close_task(v);
+    if (ok && close_k >= 0) {
+      if (nmc_wait_published(d, cb, close_k % v.P,
+                             (unsigned)v.G * (unsigned)(close_k / v.P - i0 + 1), lds,
+                             hl_view(v.L)))
+        task(v, close_k, true, false, 0, 0, 0);
+    }
+    nmc_drain_vm();
+    return;
+  }
+
+  // ---- control wave and likelihood waves ----
+  if (ctl && W > 1 && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
+  int pub_p = -1;                  // control: parameter whose sc1 value store awaits its count
+  int pend_p = -1, pend_t = 0;     // control: decided step whose state update is pending
+  double c_LL = 0.0;               // control: the group LL of the current state
+  if (ctl) {
+    const View v = view();
+    c_LL = d.ll[v.gc];
+  }
+  bool q_acc = false;
+  double q_plp = 0, q_pll = 0;
+  // the rest of a decided step's update (:369-383, :608-610): counters, log prior, LL,
+  // sample and trace rows
+  auto apply_pending = [&](const View& v) {
+    const int P = v.P, G = v.G, C = v.C;
+    const nmc_sweep_layout& L = v.L;
+    double* th = lds + L.th * 64 + lane;
+    double* st = lds + L.st * 64 + lane;
+    const double* cwv = lds + L.cw * 64 + lane;
+    const int q = pend_p, tq = pend_t;
+    st[(NMC_ST_LP * P + q) * 64] = q_plp;
+    st[(NMC_ST_NA * P + q) * 64] = cwv[(q_acc ? NMC_CW_NAA : NMC_CW_NAR) * 64];
+    st[(NMC_ST_NR * P + q) * 64] = cwv[(q_acc ? NMC_CW_NRA : NMC_CW_NRR) * 64];
+    st[(NMC_ST_TA * P + q) * 64] = cwv[NMC_CW_TA * 64] + (q_acc ? 1.0 : 0.0);
+    if (q_acc) c_LL = q_pll;
+    if (live) {
+      const int row = nmc_record_row(d, tq);
+      if (row >= 0) {
+        const int col = q * (G + (PARTIAL ? 2 : 0)) + (PARTIAL ? 2 : 0) + g;
+        d.samples[((size_t)row * d.cols + col) * C + c] = th[q * 64];
+      }
+      if (tq < d.trace_n) {
+        const size_t it = (((size_t)tq * P + q) * G + g) * C + c;
+        d.tflag[it] = q_acc ? 1 : 0;
+        d.tllp[it] = q_pll;
+      }
+    }
+    pend_p = -1;
+  };
+  auto count_published = [&]() {
+    if (pub_p >= 0) {
+      nmc_drain_vm();
+      if (lane == 0)
+        __hip_atomic_fetch_add(nmc_counter(d, cb, pub_p, g & 7), 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      pub_p = -1;
+    }
+  };
+
+  for (int t = i0; t < i1 && ok; ++t) {
+    for (int p = 0; p < d.P; ++p) {
+      A = nmc_sweep_args_at<Fam>();
+      const View v = view();
+      const int P = v.P, G = v.G, C = v.C;
+      const nmc_sweep_layout& L = v.L;
+      double* th = lds + L.th * 64 + lane;
+      double* st = lds + L.st * 64 + lane;
+      double* hy = lds + L.hyp * 64 + lane;
+      double* cwv = lds + L.cw * 64 + lane;
+      unsigned* tcnt = (unsigned*)(lds + L.flag * 64 + 4);   // tile queues by step parity
+      const Fam& fam = A->fam;
+      const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
+      const int gs = t * P + p, sp = gs & 1;
+      const bool due = PARTIAL && gs - v.lag >= v.gs0;   // the Gibbs wave has a task this step
+      const bool post_prior = due && P <= 2;             // ... whose update this step's prior needs
+      // ---- control: the pending update of step gs-1 and this step's decision operands:
+      //      the proposal, both outcomes of the counters and of the (tuned) scale, priors ----
+      double c_prop = 0, c_v = 0, c_lu = 0, c_lpc = 0, c_lpp = 0, c_sA = 0, c_sR = 0;
+      typename Fam::Reg c_reg{};
+      if (ctl) {
+        if (pend_p >= 0) apply_pending(v);
+        c_v = th[p * 64];
+        const double s = st[(NMC_ST_S * P + p) * 64];
+        c_prop = c_v + (1.0 * s) * lds[(L.zl + 2 * sp) * 64 + 2 * lane];   // propose (:304-306)
+        c_lu = lds[(L.zl + 2 * sp) * 64 + 2 * lane + 1];
+        {
+          double thp[MP];
+#pragma unroll
+          for (int q = 0; q < MP; ++q) thp[q] = q < P ? (q == p ? c_prop : th[q * 64]) : 0.0;
+          c_reg = fam.prepare(thp);
+        }
+        const double na = st[(NMC_ST_NA * P + p) * 64], nr = st[(NMC_ST_NR * P + p) * 64];
+        double naA = na + 1.0, nrA = nr, naR = na, nrR = nr + 1.0;
+        c_sA = s;
+        c_sR = s;
+        if (tune) {
+          nmc_tune(c_sA, naA, nrA);
+          nmc_tune(c_sR, naR, nrR);
+        }
+        cwv[NMC_CW_NAA * 64] = naA;
+        cwv[NMC_CW_NRA * 64] = nrA;
+        cwv[NMC_CW_NAR * 64] = naR;
+        cwv[NMC_CW_NRR * 64] = nrR;
+        cwv[NMC_CW_TA * 64] = st[(NMC_ST_TA * P + p) * 64];
+        if (!post_prior) {   // priors (:293-294)
+          if constexpr (PARTIAL) {
+            const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
+            const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
+            c_lpc = t > 0 ? nmc_norm_logpdf_r(c_v, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
+            c_lpp = nmc_norm_logpdf_r(c_prop, m, sd, isd, lsd);
+          } else {
+            c_lpc = st[(NMC_ST_LP * P + p) * 64];
+            c_lpp = nmc_sweep_prior(d.pfam[p], d.ppar + 8 * p, c_prop);
+          }
+        }
+        // the previous step's published value has had the work above to drain
+        if constexpr (PARTIAL) count_published();
+      }
+
+      // ---- every wave: the likelihood of the proposal (:615-635), tile by tile from the
+      //      step's LDS queue; entry 0 (when there is a next step) draws its variates ----
+      {
+        double thp[MP];
+#pragma unroll
+        for (int q = 0; q < MP; ++q) thp[q] = q < P ? th[q * 64] : 0.0;
+        const double prop = thp[p] + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
+                                         lds[(L.zl + 2 * sp) * 64 + 2 * lane];
+#pragma unroll
+        for (int q = 0; q < MP; ++q)
+          if (q == p) thp[q] = prop;
+        const typename Fam::Reg reg = fam.prepare(thp);
+        typename Fam::Reg preg = reg;   // paired rows: the partner lane's (lane ^ 32) values
+        if constexpr (nmc_paired_rows_ok<Fam>() && !HALF) if (d.paired) {
+          const bool hi = lane >= 32;
+#pragma unroll
+          for (int q = 0; q < MP; ++q) {
+            const nmc_pair2 e = nmc_halves(thp[q]);
+            thp[q] = hi ? e.lo : e.hi;
+          }
+          preg = fam.prepare(thp);
+        }
+        const double* lrows = lds + L.rows * 64;
+        const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
+        const int zj = tn < i1 ? 1 : 0;
+        const int nt = v.TI.nt;
+        auto grab = [&]() -> unsigned {
+          unsigned k = 0;
+          if (lane == 0)
+            k = __hip_atomic_fetch_add(tcnt + sp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          return k;
+        };
+        int kq = (int)__builtin_amdgcn_readlane(grab(), 0);
+        while (kq < nt + zj) {
+          const unsigned kn = grab();
+          if (kq < zj) {
+            put_variates(v, tn, pn, sp ^ 1);
+          } else {
+            const int k = kq - zj;
+            const int ra = v.TI.start(k), rn = v.TI.len(k);
+            double acc[Fam::NACC];
+            bool done = false;
+            if constexpr (nmc_paired_rows_ok<Fam>()) if (HALF || d.paired) {
+              nmc_ll_rows_lds<Fam, true, HALF>(fam, reg, lrows + (size_t)ra * NF, rn, acc, &preg);
+              done = true;
+            }
+            if (!done) nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * NF, rn, acc);
+#pragma unroll
+            for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = acc[j];
+          }
+          kq = (int)__builtin_amdgcn_readlane(kn, 0);
+        }
+      }
+      __syncthreads();   // A: every tile partial, the next step's variates, the Gibbs priors
+
+      // (partial pooling: the Gibbs wave's verdict is read in the same batch as the operands
+      // and checked after the decision; an aborted step's decision is never used)
+      const double verdict = due ? lds[L.flag * 64 + 1 + sp] : 0.0;
+      // ---- control: group log-likelihood of the proposal (tiles in order) and the
+      //      Metropolis decision, one chain per lane (:334-383) ----
+      if (ctl) {
+        if (lane == 0) tcnt[sp] = 0u;   // every entry is taken; the queue is reused at step +2
+        double acc[Fam::NACC];
+#pragma unroll
+        for (int j = 0; j < Fam::NACC; ++j)
+          acc[j] = nmc_sum_slots(lds + (L.part + j * NMC_NSLOT) * 64 + lane);
+        const double llp = fam.finish_fast(c_reg, acc, (long)v.ngrp, fam.gconst((long)v.ngrp));
+        if (post_prior) {   // the Gibbs wave evaluated this step's priors
+          c_lpc = cwv[NMC_CW_LPC * 64];
+          c_lpp = cwv[NMC_CW_LPP * 64];
+        }
+        const double postp = c_lpp + llp;
+        const double post = c_lpc + c_LL;
+        const double diff = postp - post;
+        bool accept;
+        if (!isfinite(post) && isfinite(postp)) accept = true;        // :347-352
+        else if (!isfinite(llp)) accept = false;                      // :354-356
+        else if (!isfinite(diff)) accept = false;                     // :358-360
+        else accept = c_lu < diff;                                    // :362-364
+        // :369-383, :608-610 (+ tune :385-437, prepared above)
+        const double vn = accept ? c_prop : c_v;
+        th[p * 64] = vn;
+        if constexpr (PARTIAL) {   // publish write-through; counted at the next step's start
+          if (live)
+            __hip_atomic_store(((t & 1) ? d.vb1 : d.vb0) + (size_t)p * G * C + v.gc, vn,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          pub_p = p;
+        }
+        st[(NMC_ST_S * P + p) * 64] = accept ? c_sA : c_sR;
+        q_acc = accept;
+        q_plp = accept ? c_lpp : c_lpc;
+        q_pll = llp;
+        pend_p = p;
+        pend_t = t;
+      }
+      if (due) {
+        ok = verdict == 2.0 * ((double)gs + 1);
+        if (!ok) break;
+      }
+      __syncthreads();   // B: the decided value is visible to every wave
+    }
+  }
+
+  NMC_RUN_SL(2);
+  A = nmc_sweep_args_at<Fam>();
+  const View v = view();
+  if (ctl) {
+    if constexpr (PARTIAL) count_published();   // the last parameter's count
+    if (pend_p >= 0) apply_pending(v);
+  }
+  // ---- epilogue: state back to HBM (control wave) ----
+  if (ctl && live && ok) {
+    const int P = v.P, G = v.G, C = v.C;
+    const double* th = lds + v.L.th * 64 + lane;
+    const double* st = lds + v.L.st * 64 + lane;
+    double* vo = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
+    for (int p = 0; p < P; ++p) {
+      const size_t ip = (size_t)p * G * C + v.gc;
+      if (!PARTIAL) vo[ip] = th[p * 64];   // (partial pooling: published write-through)
+      d.lp[ip] = st[(NMC_ST_LP * P + p) * 64];
+      d.scale[ip] = st[(NMC_ST_S * P + p) * 64];
+      d.nacc[ip] = (int)st[(NMC_ST_NA * P + p) * 64];
+      d.nrej[ip] = (int)st[(NMC_ST_NR * P + p) * 64];
+      d.tacc[ip] = (long long)st[(NMC_ST_TA * P + p) * 64];
+    }
+    d.ll[v.gc] = c_LL;
+  }
+  // ---- closing Gibbs task (partial pooling): the Gibbs wave computes it; this is the
+  //      matching barrier of its nmc_wait_published ----
+  if constexpr (PARTIAL) {
+    const int close_k = close_task(v);
+    if (ok && close_k >= 0)
+      nmc_wait_published(d, cb, close_k % v.P, (unsigned)v.G * (unsigned)(close_k / v.P - i0 + 1),
+                         lds, hl_view(v.L));
+  }
+  nmc_drain_vm();
+  NMC_RUN_SL(3);
+#undef d
+}

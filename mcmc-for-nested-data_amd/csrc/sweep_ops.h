@@ -1,0 +1,86 @@
+// sweep_ops.h -- the nmc_k_sweep launches (sweep.h), instantiated once per family in their
+// own translation units (sweep_*.hip).  Those are built with -mllvm -disable-machine-licm
+// (Makefile): left alone, the backend hoists the polynomial constants of the variate draws
+// and priors out of the persistent loop into registers for the whole launch and then spills
+// them -- 20-70 VGPRs to scratch at the kernel's 168-VGPR budget (three waves per SIMD).
+#pragma once
+#include "ctx.h"
+#include "fam_make.h"
+
+// The sweep kernel instance of a mode (for launches and occupancy queries).
+template <class Fam>
+static const void* nmc_sweep_kernel(int mode) {
+  switch (mode) {
+    case NMC_MODE_NOPOOL: return (const void*)nmc_k_sweep<Fam, NMC_MODE_NOPOOL>;
+    case NMC_MODE_SYNC_REG: return (const void*)nmc_k_sweep<Fam, NMC_MODE_SYNC_REG>;
+    case NMC_MODE_SYNC_LDS: return (const void*)nmc_k_sweep<Fam, NMC_MODE_SYNC_LDS>;
+    case NMC_MODE_HALF:   // (row pairs in every block: the host's condition)
+      if constexpr (nmc_paired_rows_ok<Fam>())
+        return (const void*)nmc_k_sweep<Fam, NMC_MODE_HALF>;
+      return nullptr;
+  }
+  return nullptr;
+}
+
+// NMC_OP_RUN / NMC_OP_CAN_PERSIST / NMC_OP_CAPACITY of a context whose loop runs nmc_k_sweep.
+template <class Fam>
+static int nmc_sweep_call_t(nmc_ctx* x, const Fam& fam, NmcCall& c) {
+  switch (c.op) {
+    case NMC_OP_RUN: {
+      const int i0 = c.i0, i1 = c.i1;
+      return nmc_run_launches(x, i0, i1, [&](int mode, const Dev& d, dim3 grid, dim3 block,
+                                             size_t lds) {
+        nmc_sweep_args<Fam> a{d, fam, i0, i1};
+        void* args[] = {&a};
+        hipLaunchKernel(nmc_sweep_kernel<Fam>(mode), grid, block, args, lds, x->stream);
+      });
+    }
+    case NMC_OP_CAN_PERSIST: {   // may every workgroup of the grid be resident at once?
+      if (const char* e = getenv("NMC_PERSIST")) {
+        c.result = atoi(e) != 0;
+        return 0;
+      }
+      int nb = 0;
+      c.result = 0;
+      const void* k = nmc_sweep_kernel<Fam>(nmc_persist_mode(x));
+      if (k && hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W,
+                                                            nmc_persist_lds(x)) == hipSuccess)
+        c.result = (int64_t)x->d.RB * x->d.G * x->d.S <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
+      return 0;
+    }
+    case NMC_OP_CAPACITY: {
+      int nb = 0;
+      const void* k = nmc_sweep_kernel<Fam>(run_mode(x));
+      if (!k || hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W,
+                                                             run_lds_bytes(x)) != hipSuccess)
+        return nmc_fail(-2, "occupancy query failed");
+      c.result = nmc_safe_blocks(x, nb) * x->ncu;
+      return 0;
+    }
+  }
+  return nmc_fail(-1, "sweep: unknown op");
+}
+
+#ifdef NMC_ONLY_NF
+#define NMC_DEFINE_SWEEP_CALL(NAME, MAKE)                                              \
+  int NAME(nmc_ctx* x, NmcCall& c) {                                                   \
+    if (x->nf == NMC_ONLY_NF) return nmc_sweep_call_t(x, MAKE<NMC_ONLY_NF>(x->llc), c); \
+    return nmc_fail(-1, "NMC_ONLY_NF build");                                          \
+  }
+#else
+#define NMC_DEFINE_SWEEP_CALL(NAME, MAKE)                                   \
+  int NAME(nmc_ctx* x, NmcCall& c) {                                        \
+    switch (x->nf) {                                                        \
+      case 1: return nmc_sweep_call_t(x, MAKE<1>(x->llc), c);               \
+      case 2: return nmc_sweep_call_t(x, MAKE<2>(x->llc), c);               \
+      case 3: return nmc_sweep_call_t(x, MAKE<3>(x->llc), c);               \
+      case 4: return nmc_sweep_call_t(x, MAKE<4>(x->llc), c);               \
+      case 5: return nmc_sweep_call_t(x, MAKE<5>(x->llc), c);               \
+      case 6: return nmc_sweep_call_t(x, MAKE<6>(x->llc), c);               \
+      case 7: return nmc_sweep_call_t(x, MAKE<7>(x->llc), c);               \
+      case 8: return nmc_sweep_call_t(x, MAKE<8>(x->llc), c);               \
+      case 9: return nmc_sweep_call_t(x, MAKE<9>(x->llc), c);               \
+    }                                                                       \
+    return nmc_fail(-1, "n_fields must be 1..9");                           \
+  }
+#endif

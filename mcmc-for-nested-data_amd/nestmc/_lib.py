@@ -92,6 +92,8 @@ SIGNATURES = {
     "nmc_debug_rng": (ctypes.c_int, [_c_uint32_p, ctypes.c_int, ctypes.c_uint32,
                                      ctypes.c_double, _c_double_p]),
     "nmc_debug_stamps": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
+    "nmc_debug_softplus": (ctypes.c_int, [_c_double_p, ctypes.c_int, _c_double_p,
+                                          ctypes.c_int]),
 }
 
 _lib = None

@@ -188,13 +188,16 @@ def test_eval_group_ll_matches_oracle(gpu_lib):
     ("regression3_none", 65, 4, 25, False, 40),     # asm loop, sigma sampled, no pooling
     ("gauss_none", 64, 6, 20, True, 30),            # generic loop, 3 fields
     ("linreg_partial", 64, 64, 256, False, 12),     # register Gibbs hand-off, G = 64
+    ("linreg_partial", 130, 100, 48, True, 12),     # LDS Gibbs payload, 64 < G <= 128
     ("logistic_partial", 96, 24, 200, True, 10),    # tails in every group
 ])
 def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
     """The paired-chain row loop (each lane evaluates its row pair half for its own chain
     and for lane ^ 32's, kernels.h nmc_ll_rows_lds<Fam, true>) reproduces the one-chain
-    broadcast loop bit for bit: flags, proposal LLs and recorded rows; so does the opt-in
-    one-barrier step kernel (step.h, where it applies)."""
+    broadcast loop bit for bit: flags, proposal LLs and recorded rows; so do nmc_k_run
+    (NMC_SWEEP=0: eight waves, every variate from the fill kernel) against the default
+    twelve-wave nmc_k_sweep (variates drawn in the kernel), and the opt-in one-barrier step
+    kernel (step.h, where it applies)."""
     from gpu_cases import run_engine
     fam, sizes, priors, pooling, names = synthetic(kind, C, G, N, ragged=ragged)
     P = fam.n_params
@@ -204,8 +207,8 @@ def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
             # none pooling on few workgroups runs the half layout (32 chains per workgroup,
             # lane pairs on the two row parities); this keeps 64 chains per workgroup
             "full": {"NMC_HALF": "0"},
-            # step variates from the fill kernel's ring, not the step kernel's variate job
-            "fill": {"NMC_ZIN": "0"},
+            # nmc_k_run (eight waves, variates from the fill kernel) instead of nmc_k_sweep
+            "run": {"NMC_SWEEP": "0"},
             # the opt-in one-barrier step kernel (step.h), both variant flags
             "step": {"NMC_STEP": "1", "NMC_STEP_FLAGS": "3"}}
     for name, env in envs.items():
@@ -214,9 +217,11 @@ def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
     if pooling != "partial":
         assert runs["paired"][3]["mode"] == "NMC_MODE_HALF", runs["paired"][3]
         assert runs["full"][3]["mode"] == "NMC_MODE_NOPOOL", runs["full"][3]
+    assert runs["paired"][3]["kernel"].startswith("nmc_k_sweep<"), runs["paired"][3]
+    assert runs["run"][3]["kernel"].startswith("nmc_k_run<"), runs["run"][3]
     for k in range(3):
         assert numpy.array_equal(runs["paired"][k], runs["bcast"][k], equal_nan=True), k
         assert numpy.array_equal(runs["paired"][k], runs["step"][k], equal_nan=True), k
         assert numpy.array_equal(runs["paired"][k], runs["full"][k], equal_nan=True), k
-        assert numpy.array_equal(runs["paired"][k], runs["fill"][k], equal_nan=True), k
+        assert numpy.array_equal(runs["paired"][k], runs["run"][k], equal_nan=True), k
     assert runs["paired"][0].mean() > 0.02
