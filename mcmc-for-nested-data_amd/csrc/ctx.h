@@ -78,7 +78,8 @@ static inline size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
 }
 static inline int run_mode(const nmc_ctx* x) {
   if (x->pooling != NMC_POOL_PARTIAL) return x->d.CL == 32 ? NMC_MODE_HALF : NMC_MODE_NOPOOL;
-  if (x->sweep) return x->d.G <= 64 ? NMC_MODE_SYNC_REG : NMC_MODE_SYNC_LDS;
+  if (x->sweep)
+    return x->d.G <= 64 ? NMC_MODE_SYNC_REG : x->d.G <= 128 ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC_OWN;
   if (!x->persistent) return NMC_MODE_LAUNCH;
   if (x->d.hreg) return x->d.hown ? NMC_MODE_SYNC_OWN : NMC_MODE_SYNC_REG;
   return x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
@@ -97,10 +98,21 @@ static inline size_t step_lds_bytes(const nmc_ctx* x) {
                               x->d.nmax * x->nf, x->d.G).total * 512;
 }
 
-// LDS of nmc_k_sweep (sweep.h)
+// LDS of nmc_k_sweep (sweep.h); partial pooling over G > 128 groups also runs the Gibbs
+// workgroups (SYNC_OWN) in the same launch: their hyper carve (nmc_lds, no rows) must fit
 static inline size_t sweep_lds_bytes(const nmc_ctx* x) {
-  return (size_t)nmc_sweep_lds(x->nacc, x->d.P, x->pooling == NMC_POOL_PARTIAL,
-                               x->d.G > 64 ? 1 : 0, x->d.G, x->d.nmax * x->nf).total * 512;
+  const Dev& d = x->d;
+  const bool partial = x->pooling == NMC_POOL_PARTIAL;
+  size_t b = (size_t)nmc_sweep_lds(x->nacc, d.P, partial, d.G > 64 && d.G <= 128 ? 1 : 0, d.G,
+                                   d.nmax * x->nf).total * 512;
+  if (partial && d.G > 128)
+    b = std::max(b, (size_t)nmc_lds(0, d.P, 1, d.nleaf, d.ntail, d.W, d.G, 0, 0).total * 512);
+  return b;
+}
+// workgroups of the sweep grid: RB * G likelihood workgroups (+ RB * P Gibbs workgroups)
+static inline int64_t sweep_grid(const nmc_ctx* x) {
+  const Dev& d = x->d;
+  return (int64_t)d.RB * d.G + (x->pooling == NMC_POOL_PARTIAL && d.G > 128 ? (int64_t)d.RB * d.P : 0);
 }
 
 static inline size_t run_lds_bytes(const nmc_ctx* x) {

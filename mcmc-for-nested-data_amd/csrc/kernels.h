@@ -372,7 +372,7 @@ __device__ __forceinline__ void nmc_drain_vm() { asm volatile("s_waitcnt vmcnt(0
 #ifndef NMC_HYPER_NS
 #define NMC_HYPER_NS 1   // streams per wave-iteration (2 and 4 measured slower at cfg 4)
 #endif
-template <int SRC, bool SQ>
+template <int SRC, bool SQ, int NS = NMC_HYPER_NS>
 __device__ __forceinline__ void nmc_hyper_streams(const Dev& d, const double* src, int cc,
                                                   double* lds, const nmc_lds_layout& L,
                                                   int ponly = -1) {
@@ -385,7 +385,6 @@ __device__ __forceinline__ void nmc_hyper_streams(const Dev& d, const double* sr
   const int sbeg = ponly < 0 ? 0 : ponly * nl * per;
   const int nst = ponly < 0 ? P * nl * per : (ponly + 1) * nl * per;
   // NS streams per wave-iteration, their loads in flight together
-  constexpr int NS = NMC_HYPER_NS;
   struct Strm {
     int j, pl, p, m, m8;
     const double* xp;
@@ -495,8 +494,10 @@ __device__ __forceinline__ void nmc_hyper_variates(const Dev& d, int cb, int t, 
 }
 
 // ponly >= 0: the update of that parameter alone (the persistent all-wave mode updates
-// parameter p at step (t + 1, p), one step after the last publication it needs)
-template <int SRC>
+// parameter p at step (t + 1, p), one step after the last publication it needs).
+// NS: streams per wave-iteration with their loads in flight together; WT: the global hyper
+// state is stored write-through (agent scope: other workgroups read it inside the launch).
+template <int SRC, int NS = NMC_HYPER_NS, bool WT = false>
 __device__ __forceinline__ void nmc_hyper(const Dev& d, const double* src, int cb, int t,
                                           double* lds, const nmc_lds_layout& L, bool write,
                                           int ponly = -1) {
@@ -508,7 +509,7 @@ __device__ __forceinline__ void nmc_hyper(const Dev& d, const double* src, int c
   const int cc = c < C ? c : C - 1;
   const bool own = nmc_lane_owns(d, c, lane);
   const int pb = ponly < 0 ? 0 : ponly, pe = ponly < 0 ? P : ponly + 1;
-  nmc_hyper_streams<SRC, false>(d, src, cc, lds, L, ponly);
+  nmc_hyper_streams<SRC, false, NS>(d, src, cc, lds, L, ponly);
   __syncthreads();
   for (int p = pb + w; p < pe; p += W) {
     const double tot = nmc_hyper_combine(d, lds, L, p, lane);
@@ -517,7 +518,7 @@ __device__ __forceinline__ void nmc_hyper(const Dev& d, const double* src, int c
     lds[(L.hyp + NMC_HY_MU * P + p) * 64 + lane] = tot / G + sdm * hz;   // mu ~ N(mean(x), sqrt(s2/G))
   }
   __syncthreads();
-  nmc_hyper_streams<SRC, true>(d, src, cc, lds, L, ponly);
+  nmc_hyper_streams<SRC, true, NS>(d, src, cc, lds, L, ponly);
   __syncthreads();
   const int row = write ? nmc_record_row(d, t) : -1;
   for (int p = pb + w; p < pe; p += W) {
@@ -536,10 +537,17 @@ __device__ __forceinline__ void nmc_hyper(const Dev& d, const double* src, int c
     lds[(L.hyp + NMC_HY_ISD * P + p) * 64 + lane] = 1.0 / sdn;
     if (write && own) {
       const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
-      d.mu[ho] = m;
-      d.s2[ho] = s2n;
-      d.hsd[ho] = sdn;
-      d.hlsd[ho] = lsd;
+      if constexpr (WT) {
+        __hip_atomic_store(d.mu + ho, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d.s2 + ho, s2n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d.hsd + ho, sdn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d.hlsd + ho, lsd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        d.mu[ho] = m;
+        d.s2[ho] = s2n;
+        d.hsd[ho] = sdn;
+        d.hlsd[ho] = lsd;
+      }
       if (row >= 0) {
         double* out = d.samples + ((size_t)row * d.cols + (size_t)p * (G + 2)) * C + c;
         out[0] = m;
@@ -1540,7 +1548,10 @@ enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
 typedef __attribute__((address_space(4))) const Dev* nmc_kdev_ptr;
 __device__ __forceinline__ const Dev* nmc_kdev() {
   nmc_kdev_ptr p = (nmc_kdev_ptr)__builtin_amdgcn_kernarg_segment_ptr();
+#ifndef NMC_STAMPS   // (the stamps build's divergent stamp stores make the backend move the
+                     //  laundered pointer to VGPRs, an illegal copy: diagnostics keep it plain)
   asm volatile("" : "+s"(p));
+#endif
   return (const Dev*)p;
 }
 

@@ -146,9 +146,12 @@ static void choose_geometry(nmc_ctx* x) {
   x->sweep = false;
   if (d.rows_lds && d.S == 1 && !x->step_ok && !x->no_sweep &&
       !(getenv("NMC_SWEEP") && !atoi(getenv("NMC_SWEEP"))) &&
-      (x->pooling != NMC_POOL_PARTIAL || (d.G <= 128 && d.nleaf == 1))) {
-    const int64_t wgs = (int64_t)d.RB * d.G;
-    int sw = wgs <= x->ncu ? NMC_SWEEP_THREADS / 64 : wgs <= 2 * (int64_t)x->ncu ? 6 : 4;
+      (x->pooling != NMC_POOL_PARTIAL || d.nleaf <= 4)) {
+    // (a multiple of four waves: a workgroup's waves spread evenly over the four SIMDs, so
+    // two or three 4-wave workgroups per CU are resident whenever the occupancy API says so)
+    const int64_t wgs = (int64_t)d.RB * d.G +
+                        (x->pooling == NMC_POOL_PARTIAL && d.G > 128 ? (int64_t)d.RB * d.P : 0);
+    int sw = wgs <= x->ncu ? NMC_SWEEP_THREADS / 64 : 4;
     if (const char* e = getenv("NMC_SWEEP_WAVES")) {
       const int v = atoi(e);
       if (v >= 3 && v <= NMC_SWEEP_THREADS / 64) sw = v;
@@ -445,6 +448,8 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   // the fill's ring); NMC_ZIN=0 keeps the fill (bit-identical; tests compare them)
   d.zin = NMC_ZIN_BUILD && !uses_step(x, run_mode(x)) &&
           !(getenv("NMC_ZIN") && !atoi(getenv("NMC_ZIN")));
+  // nmc_k_sweep: every variate drawn in the kernel (NMC_ZIN=1) or from the fill's ring
+  if (x->sweep) d.zin = getenv("NMC_ZIN") ? (atoi(getenv("NMC_ZIN")) != 0) : 0;
   d.thin = 1; d.tune_interval = 100;
   HIPCHK(hipMemcpy(off, group_offsets, (n_groups + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
   if (n_obs > 0)
@@ -644,10 +649,10 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       // every variate of iterations [c0, c1) in one fully parallel launch: the hyper
       // variates (partial pooling) and the step variates (unless the step kernel draws them)
       x->d.vbase = c0;
-      // (nmc_k_sweep draws every variate itself)
-      const size_t n = x->sweep ? 0
-                                : (size_t)(c1 - c0) * P * x->C *
-                                      ((x->d.zin ? 0 : x->G) + (partial ? 1 : 0));
+      // (nmc_k_sweep with Dev.zin draws every variate itself)
+      const size_t n = x->sweep && x->d.zin ? 0
+                                            : (size_t)(c1 - c0) * P * x->C *
+                                                  ((x->d.zin ? 0 : x->G) + (partial ? 1 : 0));
       if (n) {
         const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);
         hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);

@@ -11,12 +11,13 @@
 // on every SIMD while the roles run.  The kernel holds few values across its persistent
 // loop: Dev is read through a pointer laundered at the top of every step (nmc_kdev), and
 // each role's values live in its own branch (the Gibbs wave's 64-value payload never shares
-// registers with the row loop).  Every variate is drawn inside the kernel, so no fill
-// kernel runs before it:
+// registers with the row loop).  The variates come from nmc_k_fill's ring (the control wave
+// LDS-DMAs each next step's {z, log u}; the Gibbs wave reads its task's pair), or, with
+// Dev.zin, are drawn inside the kernel (the fill's own functions, so the same bits):
 //   * {z, log u} of step (t, p) (Parameter.propose :304-306, the accept uniform :362):
-//     entry 0 of the previous step's tile queue (nmc_step_variate, the fill's function);
+//     entry 0 of the previous step's tile queue;
 //   * {hyper z, Gamma((G-1)/2)} of a Gibbs task (HyperParameter.update :481-498): drawn by
-//     the Gibbs wave for its own task (nmc_hyper_variate, the fill's function).
+//     the Gibbs wave for its own task.
 //
 // MODE (kernels.h NMC_MODE_*):
 //   NOPOOL    none / complete pooling, 64 chains per workgroup
@@ -25,6 +26,13 @@
 //             into registers (one sc1 round trip) -- nmc_k_run's register hand-off
 //   SYNC_LDS  partial pooling, 64 < G <= 128 (one numpy leaf): the same hand-off with the
 //             payload moved to LDS by LDS-DMA, updated from there (nmc_hyper_compute)
+//   SYNC_OWN  partial pooling, G > 128 (up to four numpy leaves): RB * P extra workgroups in
+//             the grid, one per (chain block, parameter), compute each Gibbs task ONCE for the
+//             chain block (every wave streaming its numpy streams' values with sc1 loads, all
+//             in flight; nmc_hyper) and publish the four hyper values write-through with a
+//             ready count; each likelihood workgroup's Gibbs wave only polls that count and
+//             reads the four values (nmc_hyper_read) -- instead of every one of the G
+//             workgroups streaming the chain block's G values itself
 // Wave roles per step k = (t, p):
 //   wave 0   control: the deferred state update of step k-1, the decision's operands (both
 //            counter outcomes, tuned scales, priors), the count of the last published value;
@@ -133,12 +141,14 @@ template <class Fam, int MODE>
 __global__ void __launch_bounds__(NMC_SWEEP_THREADS)
 nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
   (void)a_arg;   // (read through nmc_sweep_args_at(): the same bytes)
-  constexpr bool PARTIAL = MODE == NMC_MODE_SYNC_REG || MODE == NMC_MODE_SYNC_LDS;
+  constexpr bool OWN = MODE == NMC_MODE_SYNC_OWN;
+  constexpr bool PARTIAL = MODE == NMC_MODE_SYNC_REG || MODE == NMC_MODE_SYNC_LDS || OWN;
   constexpr bool HREG = MODE == NMC_MODE_SYNC_REG;
   constexpr bool HALF = MODE == NMC_MODE_HALF;
   constexpr int NF = Fam::NFIELDS;
   constexpr int MP = Fam::MAXP;
   static_assert(MODE == NMC_MODE_NOPOOL || MODE == NMC_MODE_HALF || PARTIAL, "sweep modes");
+  (void)OWN;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const nmc_sweep_args<Fam>* A = nmc_sweep_args_at<Fam>();
 #define d (A->d)
@@ -146,6 +156,57 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int W = blockDim.x >> 6;
   const int i0 = A->i0, i1 = A->i1;
+
+  // ---- SYNC_OWN: the Gibbs workgroups (blocks RB * G ..), one per (chain block, parameter q):
+  //      every task (t, q) of the launch in order, once its publication is complete ----
+  if constexpr (OWN) if ((int)blockIdx.x >= d.RB * d.G) {
+    const int kb = (int)blockIdx.x - d.RB * d.G;
+    const int P = d.P, G = d.G, C = d.C;
+    const int hcb = kb / P, q = kb % P;
+    const int c = hcb * 64 + lane;
+    const int cc = c < C ? c : C - 1;
+    const nmc_lds_layout H = nmc_lds(0, P, 1, d.nleaf, d.ntail, W, G, 0, 0);
+    double* hy = lds + H.hyp * 64 + lane;
+    if (w == 0) {   // the state of q after iteration i0-1 (slot (i0-1) & 1)
+      const size_t ho = nmc_hslot(d, i0 - 1) + (size_t)q * C + cc;
+      hy[(NMC_HY_MU * P + q) * 64] = d.mu[ho];
+      hy[(NMC_HY_SD * P + q) * 64] = d.hsd[ho];
+      hy[(NMC_HY_LSD * P + q) * 64] = d.hlsd[ho];
+      hy[(NMC_HY_S2 * P + q) * 64] = d.s2[ho];
+    }
+    for (int t = i0; t < i1; ++t) {
+      A = nmc_sweep_args_at<Fam>();
+      if (!nmc_wait_published(d, hcb, q, (unsigned)d.G * (unsigned)(t - i0 + 1), lds, H)) break;
+      if (w == 0) {   // the task's variates and sqrt(s2 / G) of the previous update
+        nmc_d2 hv;
+        if (d.zin) {
+          hv = nmc_sweep_hyper_variate(d.rhz, d.rhu, d.replay_n, d.rng_mode, d.P, d.C,
+                                       (uint32_t)(d.chain_base + cc), d.seed, d.ha, d.hlga, t, q,
+                                       cc);
+        } else {
+          const size_t hvi = (((size_t)(t - d.vbase) * d.P + q) * d.C + cc) * 2;
+          hv.a = d.vh[hvi];
+          hv.b = d.vh[hvi + 1];
+        }
+        lds[H.hv * 64 + (q * 64 + lane) * 2] = hv.a;
+        lds[H.hv * 64 + (q * 64 + lane) * 2 + 1] = hv.b;
+        hy[(NMC_HY_SDM * d.P + q) * 64] = sqrt(hy[(NMC_HY_S2 * d.P + q) * 64] / d.G);
+      }
+      __syncthreads();
+      // HyperParameter.update (:463-498) for the chain block, written through to the global
+      // slot of t (and the sample row); wave 0 stored it and counts it ready
+      nmc_hyper<NMC_SRC_SC1, 4, true>(d, (t & 1) ? d.vb1 : d.vb0, hcb, t, lds, H, true, q);
+      if (w == 0) {
+        nmc_drain_vm();
+        if (lane == 0)
+          __hip_atomic_fetch_add(nmc_hrd(d, hcb, q), 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    nmc_drain_vm();
+    return;
+  }
+
   const int g = blockIdx.x % d.G, cb = blockIdx.x / d.G;
   const int c = HALF ? cb * 32 + (lane & 31) : cb * 64 + lane;
   const bool live = c < d.C && (!HALF || lane < 32);   // writes this lane's outputs
@@ -182,14 +243,23 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
   // the task this workgroup closes after the loop: ge-lag+g (groups 0 .. lag-1), -1: none
   auto close_task = [&](const View& v) {
     const int k0 = v.ge - v.lag > v.gs0 ? v.ge - v.lag : v.gs0;
-    return PARTIAL && k0 + g < v.ge ? k0 + g : -1;
+    return PARTIAL && !OWN && k0 + g < v.ge ? k0 + g : -1;
   };
   // {z, log u} of step (tn, pn) -> LDS slot `slot` (this lane's chain)
+  // d.zin: drawn here; otherwise the LDS-DMA of the pair nmc_k_fill wrote to the ring vzl
+  // (the issuing wave drains its vmcnt before the next barrier)
   auto put_variates = [&](const View& v, int tn, int pn, int slot) {
-    const nmc_d2 r = nmc_sweep_step_variate(d.rz, d.ru, d.replay_n, d.rng_mode, v.P, v.G, v.C,
-                                            (uint32_t)(d.chain_base + cc), d.seed, tn, pn, g, cc);
-    lds[(v.L.zl + 2 * slot) * 64 + 2 * lane] = r.a;
-    lds[(v.L.zl + 2 * slot) * 64 + 2 * lane + 1] = r.b;
+    if (d.zin) {
+      const nmc_d2 r = nmc_sweep_step_variate(d.rz, d.ru, d.replay_n, d.rng_mode, v.P, v.G, v.C,
+                                              (uint32_t)(d.chain_base + cc), d.seed, tn, pn, g,
+                                              cc);
+      lds[(v.L.zl + 2 * slot) * 64 + 2 * lane] = r.a;
+      lds[(v.L.zl + 2 * slot) * 64 + 2 * lane + 1] = r.b;
+    } else {
+      nmc_dma16(d.vzl + ((size_t)(tn - d.vbase) * v.P * v.G * v.C + (size_t)pn * v.G * v.C +
+                         v.gc) * 2,
+                lds + (v.L.zl + 2 * slot) * 64);
+    }
   };
 
   NMC_RUN_SL(0);
@@ -256,30 +326,45 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
       const int P = v.P, G = v.G, C = v.C;
       const nmc_sweep_layout& L = v.L;
       const int kq = k % P, kt = k / P;
-      const bool r = nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1));
-      if (!r) return false;
+      if constexpr (OWN) {   // the Gibbs workgroup of (cb, kq) has counted task k ready
+        if (!nmc_poll_count(d, nmc_hrd(d, cb, kq), (unsigned)(kt - i0 + 1) + d.pbase))
+          return false;
+      } else {
+        if (!nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1))) return false;
+      }
       // keep the payload loads below the poll (no instruction: wavefront scope)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const nmc_d2 hv = nmc_sweep_hyper_variate(d.rhz, d.rhu, d.replay_n, d.rng_mode, P, C,
-                                                (uint32_t)(d.chain_base + cc), d.seed, d.ha,
-                                                d.hlga, kt, kq, cc);
-      if constexpr (HREG) {
-        double xv[64];
-        const double* src = ((kt & 1) ? d.vb1 : d.vb0) + (size_t)kq * G * C + cc;
-#pragma unroll
-        for (int u = 0; u < 64; ++u) xv[u] = nmc_ldv<NMC_SRC_SC1>(src + (size_t)u * C);
-        nmc_hyper_compute_reg(d, cb, kt, kq, lds, L.hyp, write, hv.a, hv.b, xv);
+      if constexpr (OWN) {
+        nmc_hyper_read(d, kt, kq, cc, lds, L.hyp);
       } else {
-        const nmc_lds_layout H = hl_view(L);
-        const double* src = (kt & 1) ? d.vb1 : d.vb0;
-        if ((C & 1) == 0) {
-          nmc_hyper_dma(d, src, kq, cb, 0, G, lds, H, 0);
-          nmc_drain_vm();
-        } else {
-          nmc_hyper_load(d, src, kq, cc, 0, G, lds, H, 0);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        nmc_d2 hv;
+        if (d.zin) {
+          hv = nmc_sweep_hyper_variate(d.rhz, d.rhu, d.replay_n, d.rng_mode, P, C,
+                                       (uint32_t)(d.chain_base + cc), d.seed, d.ha, d.hlga, kt, kq,
+                                       cc);
+        } else {   // the fill kernel's pair
+          const size_t hvi = (((size_t)(kt - d.vbase) * P + kq) * C + cc) * 2;
+          hv.a = d.vh[hvi];
+          hv.b = d.vh[hvi + 1];
         }
-        nmc_hyper_compute(d, cb, kt, kq, lds, H, write, hv.a, hv.b, 0);
+        if constexpr (HREG) {
+          double xv[64];
+          const double* src = ((kt & 1) ? d.vb1 : d.vb0) + (size_t)kq * G * C + cc;
+#pragma unroll
+          for (int u = 0; u < 64; ++u) xv[u] = nmc_ldv<NMC_SRC_SC1>(src + (size_t)u * C);
+          nmc_hyper_compute_reg(d, cb, kt, kq, lds, L.hyp, write, hv.a, hv.b, xv);
+        } else {
+          const nmc_lds_layout H = hl_view(L);
+          const double* src = (kt & 1) ? d.vb1 : d.vb0;
+          if ((C & 1) == 0) {
+            nmc_hyper_dma(d, src, kq, cb, 0, G, lds, H, 0);
+            nmc_drain_vm();
+          } else {
+            nmc_hyper_load(d, src, kq, cc, 0, G, lds, H, 0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          }
+          nmc_hyper_compute(d, cb, kt, kq, lds, H, write, hv.a, hv.b, 0);
+        }
       }
       if (priors) {   // the update lands in the step that needs it: this step's priors
         const double* th = lds + L.th * 64 + lane;
@@ -382,6 +467,7 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
   };
 
   for (int t = i0; t < i1 && ok; ++t) {
+    NMC_STAMP(t, 0);
     for (int p = 0; p < d.P; ++p) {
       A = nmc_sweep_args_at<Fam>();
       const View v = view();
@@ -439,6 +525,10 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         }
         // the previous step's published value has had the work above to drain
         if constexpr (PARTIAL) count_published();
+        {   // the next step's {z, log u} from the fill's ring (d.zin: a queue job instead)
+          const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
+          if (tn < i1 && !d.zin) put_variates(v, tn, pn, sp ^ 1);
+        }
       }
 
       // ---- every wave: the likelihood of the proposal (:615-635), tile by tile from the
@@ -465,7 +555,7 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         }
         const double* lrows = lds + L.rows * 64;
         const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
-        const int zj = tn < i1 ? 1 : 0;
+        const int zj = tn < i1 && d.zin ? 1 : 0;   // (the fill's ring: the control wave's DMA)
         const int nt = v.TI.nt;
         auto grab = [&]() -> unsigned {
           unsigned k = 0;
@@ -494,7 +584,10 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
           kq = (int)__builtin_amdgcn_readlane(kn, 0);
         }
       }
+      if (ctl) nmc_drain_vm();   // (its variate DMA has landed)
+      NMC_STAMP(t, 1 + 3 * (p & 1));
       __syncthreads();   // A: every tile partial, the next step's variates, the Gibbs priors
+      NMC_STAMP(t, 2 + 3 * (p & 1));
 
       // (partial pooling: the Gibbs wave's verdict is read in the same batch as the operands
       // and checked after the decision; an aborted step's decision is never used)
@@ -540,8 +633,10 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         ok = verdict == 2.0 * ((double)gs + 1);
         if (!ok) break;
       }
+      if (p == 0) NMC_STAMP(t, 3);
       __syncthreads();   // B: the decided value is visible to every wave
     }
+    NMC_STAMP(t, 6);
   }
 
   NMC_RUN_SL(2);

@@ -14,6 +14,7 @@ static const void* nmc_sweep_kernel(int mode) {
     case NMC_MODE_NOPOOL: return (const void*)nmc_k_sweep<Fam, NMC_MODE_NOPOOL>;
     case NMC_MODE_SYNC_REG: return (const void*)nmc_k_sweep<Fam, NMC_MODE_SYNC_REG>;
     case NMC_MODE_SYNC_LDS: return (const void*)nmc_k_sweep<Fam, NMC_MODE_SYNC_LDS>;
+    case NMC_MODE_SYNC_OWN: return (const void*)nmc_k_sweep<Fam, NMC_MODE_SYNC_OWN>;
     case NMC_MODE_HALF:   // (row pairs in every block: the host's condition)
       if constexpr (nmc_paired_rows_ok<Fam>())
         return (const void*)nmc_k_sweep<Fam, NMC_MODE_HALF>;
@@ -32,7 +33,9 @@ static int nmc_sweep_call_t(nmc_ctx* x, const Fam& fam, NmcCall& c) {
                                              size_t lds) {
         nmc_sweep_args<Fam> a{d, fam, i0, i1};
         void* args[] = {&a};
-        hipLaunchKernel(nmc_sweep_kernel<Fam>(mode), grid, block, args, lds, x->stream);
+        // (SYNC_OWN: the Gibbs workgroups after the likelihood ones)
+        const dim3 gr(mode == NMC_MODE_SYNC_OWN ? (unsigned)sweep_grid(x) : grid.x);
+        hipLaunchKernel(nmc_sweep_kernel<Fam>(mode), gr, block, args, lds, x->stream);
       });
     }
     case NMC_OP_CAN_PERSIST: {   // may every workgroup of the grid be resident at once?
@@ -45,7 +48,7 @@ static int nmc_sweep_call_t(nmc_ctx* x, const Fam& fam, NmcCall& c) {
       const void* k = nmc_sweep_kernel<Fam>(nmc_persist_mode(x));
       if (k && hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W,
                                                             nmc_persist_lds(x)) == hipSuccess)
-        c.result = (int64_t)x->d.RB * x->d.G * x->d.S <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
+        c.result = sweep_grid(x) <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
       return 0;
     }
     case NMC_OP_CAPACITY: {

@@ -25,10 +25,10 @@ namespace {
 // kernel table entries, in name-expression order
 // (nmc_k_run: mode m (0..5) with rows in LDS at UK_RUN0 + m, rows staged at UK_RUN0 + 6 + m;
 // nmc_k_step: NOPOOL / SYNC_REG at UK_STEP0 / UK_STEP0 + 1; the half layout at UK_HALF)
-// (nmc_k_sweep: NOPOOL / SYNC_REG / SYNC_LDS / HALF at UK_SWEEP0 + 0..3)
+// (nmc_k_sweep: NOPOOL / SYNC_REG / SYNC_LDS / HALF / SYNC_OWN at UK_SWEEP0 + 0..4)
 enum { UK_RUN0 = 0, UK_NRUN = 6, UK_GROUP_LL = 12, UK_OBS_LL_ROWS = 13, UK_OBS_LL = 14,
        UK_STEP0 = 15, UK_GROUP_LL_RL = 17, UK_GROUP_FIN = 18, UK_HALF = 19, UK_SWEEP0 = 20,
-       UK_N = 24 };
+       UK_N = 25 };
 const char* const kNames[UK_N] = {
     "nmc_k_run<FamUser, 0, true>", "nmc_k_run<FamUser, 1, true>", "nmc_k_run<FamUser, 2, true>",
     "nmc_k_run<FamUser, 3, true>", "nmc_k_run<FamUser, 4, true>", "nmc_k_run<FamUser, 5, true>",
@@ -39,11 +39,11 @@ const char* const kNames[UK_N] = {
     "nmc_k_obs_ll<FamUser>", "nmc_k_step<FamUser, 0>", "nmc_k_step<FamUser, 4>",
     "nmc_k_group_part<FamUser, true>", "nmc_k_group_fin<FamUser>",
     "nmc_k_run<FamUser, 6, true>", "nmc_k_sweep<FamUser, 0>", "nmc_k_sweep<FamUser, 4>",
-    "nmc_k_sweep<FamUser, 3>", "nmc_k_sweep<FamUser, 6>"};
+    "nmc_k_sweep<FamUser, 3>", "nmc_k_sweep<FamUser, 6>", "nmc_k_sweep<FamUser, 5>"};
 int run_index(const nmc_ctx* x, int mode) {
   if (x->sweep)
     return UK_SWEEP0 + (mode == NMC_MODE_NOPOOL ? 0 : mode == NMC_MODE_SYNC_REG ? 1
-                        : mode == NMC_MODE_SYNC_LDS ? 2 : 3);
+                        : mode == NMC_MODE_SYNC_LDS ? 2 : mode == NMC_MODE_HALF ? 3 : 4);
   if (uses_step(x, mode)) return UK_STEP0 + (mode == NMC_MODE_NOPOOL ? 0 : 1);
   if (mode == NMC_MODE_HALF) return UK_HALF;
   return UK_RUN0 + mode + (x->d.rows_lds ? 0 : UK_NRUN);
@@ -218,7 +218,8 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
         void* sargs[] = {&sa};
         hipFunction_t fr = nullptr;
         rc = user_fn(x, run_index(x, mode), &fr);
-        if (!rc) rc = launch(x, fr, grid, block, lds, x->sweep ? sargs : args);
+        const dim3 gr(x->sweep && mode == NMC_MODE_SYNC_OWN ? (unsigned)sweep_grid(x) : grid.x);
+        if (!rc) rc = launch(x, fr, gr, block, lds, x->sweep ? sargs : args);
       });
       return rc ? rc : e;
     }
@@ -234,7 +235,8 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
         c.result = 0;
         return 0;
       }
-      c.result = (int64_t)x->d.RB * x->d.G * x->d.S <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
+      c.result = (x->sweep ? sweep_grid(x) : (int64_t)x->d.RB * x->d.G * x->d.S) <=
+                 (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
       return 0;
     }
     case NMC_OP_CAPACITY: {

@@ -46,13 +46,22 @@ def test_cfg4_geometry_multileaf_gibbs(gpu_lib, G):
     sizes = [N] * G
     C = 128
     st, nested = partial_state(fam, sizes, C, 2)
-    # one chain block: G workgroups, co-resident -> persistent (SYNC, multi-leaf plan)
+    # one chain block: G workgroups + P Gibbs workgroups, co-resident -> persistent
+    # (nmc_k_sweep SYNC_OWN: each task computed once per chain block by its Gibbs
+    # workgroup, multi-leaf plan, read by every likelihood workgroup)
     one = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed)
     assert one[3]["persistent"], one[3]
-    # the opt-in owner hand-off (task k updated once per chain block by group k % G's
+    assert one[3]["kernel"].startswith("nmc_k_sweep<"), one[3]
+    assert one[3]["mode"] == "NMC_MODE_SYNC_OWN", one[3]
+    # nmc_k_run's all-wave update (every workgroup streams the G values after barrier A)
+    syn = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed, env={"NMC_SWEEP": "0"})
+    assert syn[3]["mode"] == "NMC_MODE_SYNC", syn[3]
+    # nmc_k_run's opt-in owner hand-off (task k updated once per chain block by group k % G's
     # Gibbs wave, the others read its four results; measured slower, kept bit-identical)
-    own = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed, env={"NMC_HOWN": "1"})
+    own = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed,
+                     env={"NMC_HOWN": "1", "NMC_SWEEP": "0"})
     assert own[3]["mode"] == "NMC_MODE_SYNC_OWN", own[3]
+    assert own[3]["kernel"].startswith("nmc_k_run<"), own[3]
     # the same chains in a two-block launch (two 4-wave workgroups per CU, persistent) and
     # forced launch per iteration
     two = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed)
@@ -61,10 +70,14 @@ def test_cfg4_geometry_multileaf_gibbs(gpu_lib, G):
     # owner hand-off in launches of 3, 3 and 2 iterations (each launch's closing task,
     # counters carried over between launches)
     spl = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, launch_iters=3,
-                     env={"NMC_HOWN": "1"})
+                     env={"NMC_HOWN": "1", "NMC_SWEEP": "0"})
+    # the sweep kernel's Gibbs workgroups over launches of 3, 3 and 2 iterations
+    swl = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, launch_iters=3)
     for k in range(3):
         assert numpy.array_equal(one[k], two[k][:64], equal_nan=True), k
         assert numpy.array_equal(one[k], own[k], equal_nan=True), k
+        assert numpy.array_equal(one[k], syn[k], equal_nan=True), k
+        assert numpy.array_equal(two[k], swl[k], equal_nan=True), k
         assert numpy.array_equal(two[k], lau[k], equal_nan=True), k
         assert numpy.array_equal(two[k], spl[k], equal_nan=True), k
     assert 0.05 < lau[0].mean() < 0.95
