@@ -53,7 +53,10 @@ LDS_PEAK_GBS = 256.0 * 256 * 2.4   # 256 B/clk/CU (ds_read_b64/b128) x 256 CUs x
 #                    paired asm loop (24 per 8-row block for two chains per lane), the
 #                    broadcast asm loop and the C++ loop alike
 #   FamGaussMean<F>  per field: theta - m (add), fma(e, e, acc) = 2F
-VALU_PER_CHAIN_ROW = {"FamLinreg<2>": 3, "FamGaussMean<3>": 6}
+#   FamUser (cfg5)   the LOGISTIC8 row below: 7-fma dot product, y * eta, and
+#                    logaddexp(0, eta) by csrc/softplus.h: 63 fp64 instructions
+#                    (profiles/isa_r04_logistic8_row.txt)
+VALU_PER_CHAIN_ROW = {"FamLinreg<2>": 3, "FamGaussMean<3>": 6, ("cfg5", "FamUser"): 63}
 
 LOGISTIC8 = r"""
 __device__ double nmc_user_loglik(const double* th, const double* row, const double* k) {
@@ -450,7 +453,7 @@ def main():
     # The binding resource is fp64 VALU issue: the lane-instructions of the shipped row loop
     # per (chain, row, parameter step), counted in its ISA for this family instance (null
     # for an instance whose loop has not been counted)
-    per_row = VALU_PER_CHAIN_ROW.get(inst)
+    per_row = VALU_PER_CHAIN_ROW.get(inst, VALU_PER_CHAIN_ROW.get((args.workload, inst)))
     if per_row is not None:
         lane_instr_per_launch = C * G * P * N * per_row * iters_per_launch
         valu_tips = lane_instr_per_launch / (avg_step_ms * 1e-3) / 1e12

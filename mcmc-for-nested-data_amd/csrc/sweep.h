@@ -388,8 +388,10 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         const View v = view();
         const int gs = t * v.P + p, sp = gs & 1;
         const bool due = gs - v.lag >= v.gs0;
+        if (p == 0) NMC_STAMP_AUX(t, 13);
         if (due) {
           const bool r = task(v, gs - v.lag, g0w, v.P <= 2, p, sp, t);
+          if (p == 0) NMC_STAMP_AUX(t, 14);
           if (lane == 0)
             __hip_atomic_store(lds + v.L.flag * 64 + 1 + sp,
                                r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
@@ -488,6 +490,12 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
       double c_prop = 0, c_v = 0, c_lu = 0, c_lpc = 0, c_lpp = 0, c_sA = 0, c_sR = 0;
       typename Fam::Reg c_reg{};
       if (ctl) {
+        {   // the next step's {z, log u} from the fill's ring, in flight first: its latency
+            // overlaps everything below (d.zin: a queue job instead).  The slot held step
+            // gs-1's pair, read by every wave before barrier B of gs-1.
+          const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
+          if (tn < i1 && !d.zin) put_variates(v, tn, pn, sp ^ 1);
+        }
         if (pend_p >= 0) apply_pending(v);
         c_v = th[p * 64];
         const double s = st[(NMC_ST_S * P + p) * 64];
@@ -523,14 +531,9 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
             c_lpp = nmc_sweep_prior(d.pfam[p], d.ppar + 8 * p, c_prop);
           }
         }
-        // the previous step's published value has had the work above to drain
-        if constexpr (PARTIAL) count_published();
-        {   // the next step's {z, log u} from the fill's ring (d.zin: a queue job instead)
-          const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
-          if (tn < i1 && !d.zin) put_variates(v, tn, pn, sp ^ 1);
-        }
       }
 
+      if (p == 0) NMC_STAMP(t, 8);   // (control: its pre-work done)
       // ---- every wave: the likelihood of the proposal (:615-635), tile by tile from the
       //      step's LDS queue; entry 0 (when there is a next step) draws its variates ----
       {
@@ -564,6 +567,9 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
           return k;
         };
         int kq = (int)__builtin_amdgcn_readlane(grab(), 0);
+        // control: the count of the previous step's published value waits until its store
+        // has drained -- after this wave's first queue entry, not on the step's critical path
+        bool pubdue = PARTIAL && ctl && pub_p >= 0;
         while (kq < nt + zj) {
           const unsigned kn = grab();
           if (kq < zj) {
@@ -581,10 +587,17 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
 #pragma unroll
             for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = acc[j];
           }
+          if constexpr (PARTIAL) if (pubdue) {
+            count_published();
+            pubdue = false;
+          }
           kq = (int)__builtin_amdgcn_readlane(kn, 0);
         }
+        if constexpr (PARTIAL) if (pubdue) count_published();   // (no entry was left)
       }
+      if (p == 0) NMC_STAMP(t, 9);
       if (ctl) nmc_drain_vm();   // (its variate DMA has landed)
+      if (p == 0) NMC_STAMP(t, 10);
       NMC_STAMP(t, 1 + 3 * (p & 1));
       __syncthreads();   // A: every tile partial, the next step's variates, the Gibbs priors
       NMC_STAMP(t, 2 + 3 * (p & 1));

@@ -2,7 +2,7 @@
 """Phase timing of the step kernel from the diagnostic stamps build (diagnostics).
 
     make -C mcmc-for-nested-data_amd/csrc stamps
-    python tools/stamps.py [none|partial] [N] [waves]
+    python tools/stamps.py [none|partial] [N] [waves] [chains] [groups]
 
 Shader-clock stamps, workgroups 0 and last, waves 0 and W-1, 8 iterations of one
 launch.  Slots: 0 iteration start, 1/4 step-0/1 likelihood done, 2/5 after the
@@ -28,7 +28,9 @@ def main():
     pooling = sys.argv[1] if len(sys.argv) > 1 else "partial"
     N = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
     waves = int(sys.argv[3]) if len(sys.argv) > 3 else 0
-    eng, fam = engine_for("linreg", 256, 64, N, pooling, waves)
+    C = int(sys.argv[4]) if len(sys.argv) > 4 else 256
+    G = int(sys.argv[5]) if len(sys.argv) > 5 else 64
+    eng, fam = engine_for("linreg", C, G, N, pooling, waves)
     eng.set_schedule(400, 400, 1)
     eng.run(0, 100)
     eng.synchronize()
