@@ -124,6 +124,12 @@ def rank_chains(wl, world, rank):
     return shard(wl["chains"], world, rank)
 
 
+def job_chains(wl, world):
+    """Chains the whole job runs: ``chains`` per rank (weak) or in total (strong); the
+    ranks' rank_chains blocks tile [0, job_chains) exactly (tests/test_bench_shard.py)."""
+    return wl["chains"] * world if wl["scaling"] == "weak" else wl["chains"]
+
+
 def make_problem(wl):
     """(family, names, priors, ranges) of a workload, data regenerated from its seed."""
     import scipy.stats
@@ -413,7 +419,7 @@ def main():
     ev_ms = eng.event_elapsed_ms(0, 1)
     t_rank = max(wall, ev_ms / 1e3)
     t_max = parallel.max_over_ranks(t_rank, hg)
-    c_total = C * world if wl["scaling"] == "weak" else wl["chains"]
+    c_total = job_chains(wl, world)
 
     # second pass, same length: per-launch events on the engine's stream -> the
     # step kernel's average duration for the roofline

@@ -170,6 +170,10 @@ int nmc_split_config(nmc_ctx* ctx, int* members, int* chain_blocks_per_launch);
 /* The step kernel a run launches, e.g. "nmc_k_step<FamLinreg<2>, NMC_MODE_SYNC_REG>"
  * (NUL-terminated, truncated to cap bytes); for the profiles and the bench report.    */
 int nmc_kernel_name(nmc_ctx* ctx, char* out, int cap);
+/* Where a run's per-step variates come from: *in_kernel = 1 when the step kernel draws
+ * them itself (no nmc_k_fill launch for them), 0 when nmc_k_fill writes them to a ring in
+ * HBM first.  Both give the same bits (Parameter.propose :304-306, the accept draw :362). */
+int nmc_variate_source(nmc_ctx* ctx, int* in_kernel);
 
 /* Sampler._printSample (:902-905) + _print (:933-936): append rows of local
  * chain c to a CSV file with the reference's "%i,%i,%f,..." formatting (and the

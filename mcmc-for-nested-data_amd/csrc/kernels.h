@@ -101,16 +101,21 @@ struct Dev {
   int noprio;            // diagnostics: no issue priority for the latency-bound waves
   int sflags;            // nmc_k_step variants (bit-identical; NMC_STEP_FLAGS): 1 Gibbs payload
                          // via LDS-DMA, 2 next proposal formed before the barrier
+  int ctiles;            // nmc_k_sweep, the control wave in the tile queue (NMC_CTL_TILES):
+                         // 0 never, 1 only while the other waves have more than a round of
+                         // entries left (default), 2 like every other wave
   int rows_lds;          // 1: each workgroup stages its group's rows in LDS once per launch
   int tile;              // target rows per likelihood tile (nmc_tiles)
-  unsigned* cnt;         // [CB][P][32] publish counters (persistent partial), zeroed per launch
+  unsigned* cnt;         // [CB][P][32] publish counters (persistent partial): zeroed at create,
+                         // then they keep counting across launches (targets offset by pbase);
+                         // reset only before pbase would overflow (nestmc.hip nmc_run)
   unsigned* tmo;         // timeout word: pinned host memory, mapped (host reads it directly)
   // variates of iterations [vbase, vbase + vcap): filled by nmc_k_fill
   double* vzl;           // [t][P][G][C][2] {proposal normal, log accept uniform}
-  // zin (build option NMC_ZIN_BUILD=1, measured slower): nmc_k_run draws each step's
-  // {z, log u} itself (nmc_step_variate, a job in the step's tile queue) and nmc_k_fill
-  // writes only the hyper variates; 0: the fill writes vzl and the control wave copies it
-  // into LDS
+  // zin: the step's {z, log u} are drawn inside the step kernel (jobs in the step's tile
+  // queue) and nmc_k_fill is not launched (nmc_k_sweep: every variate, NMC_ZIN=1; nmc_k_run:
+  // build option NMC_ZIN_BUILD=1 only, the fill still writes vh); 0: nmc_k_fill writes vzl
+  // (+ vh) and the control wave DMAs each step's pair into LDS
   int zin;
   double* vh;            // [t][P][C][2]    {hyper mean normal, hyper Gamma(a) draw}
   int vbase, vcap;

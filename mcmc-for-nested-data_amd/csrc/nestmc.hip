@@ -88,6 +88,7 @@ static void choose_geometry(nmc_ctx* x) {
   // the persistent Gibbs update by the auxiliary waves needs G <= 128 (one numpy
   // leaf) and one parameter's chain-block values in LDS
   d.noprio = getenv("NMC_NOPRIO") ? atoi(getenv("NMC_NOPRIO")) : 0;   // diagnostics bits
+  d.ctiles = getenv("NMC_CTL_TILES") ? atoi(getenv("NMC_CTL_TILES")) : 1;   // (Dev.ctiles)
   d.hlds = d.naux > 0 && d.G <= 128 && lds_bytes_for(x, 1, d.rows_lds) <= (size_t)160 * 1024 &&
            !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
   // G <= 64: the Gibbs wave fetches a task's values into registers (one sc1 round trip)
@@ -868,6 +869,12 @@ int nmc_kernel_name(nmc_ctx* x, char* out, int cap) {
                             (x->d.rows_lds ? "true" : "false") + ">";
   if (cap < 1) return fail(-1, "kernel name: cap < 1");
   snprintf(out, (size_t)cap, "%s", k.c_str());
+  return 0;
+}
+
+int nmc_variate_source(nmc_ctx* x, int* in_kernel) {
+  if (!in_kernel) return fail(-1, "variate source: null output");
+  *in_kernel = x->d.zin ? 1 : 0;
   return 0;
 }
 

@@ -15,7 +15,7 @@
 // LDS-DMAs each next step's {z, log u}; the Gibbs wave reads its task's pair), or, with
 // Dev.zin, are drawn inside the kernel (the fill's own functions, so the same bits):
 //   * {z, log u} of step (t, p) (Parameter.propose :304-306, the accept uniform :362):
-//     entry 0 of the previous step's tile queue;
+//     entries 0-2 of the previous step's tile queue (radius, cosine, log u);
 //   * {hyper z, Gamma((G-1)/2)} of a Gibbs task (HyperParameter.update :481-498): drawn by
 //     the Gibbs wave for its own task.
 //
@@ -57,6 +57,9 @@ struct nmc_sweep_layout {
   int hyp;    // [6][P]         hyper state (NMC_HY_*), partial pooling
   int hval;   // [G + 1]        SYNC_LDS: the Gibbs payload (+1: the DMA moves group pairs)
   int zl;     // [2][2]         {z, log u} of this and the next step (step parity)
+  int zm;     // [2]            the proposal normal's second factor by step parity: z is
+              //                zl's z times zm (1.0 with the fill's ring; with Dev.zin the
+              //                Box-Muller radius and cosine are two queue jobs)
   int cw;     // [8]            control values across the barriers (NMC_CW_*)
   int flag;   // [1]            word 0 wait flag, words 1-2 Gibbs verdict by step parity,
               //                uint32 words 8-9 the tile queues by step parity
@@ -72,7 +75,8 @@ __host__ __device__ inline nmc_sweep_layout nmc_sweep_lds(int nacc, int P, int p
   L.hyp = L.st + 5 * P;
   L.hval = L.hyp + (partial ? 6 * P : 0);
   L.zl = L.hval + (partial && hlds ? G + 1 : 0);
-  L.cw = L.zl + 4;
+  L.zm = L.zl + 4;
+  L.cw = L.zm + 2;
   L.flag = L.cw + 8;
   L.rows = L.flag + 1;
   // (+1 column: the pipelined likelihood loop prefetches one block past a wave's rows)
@@ -83,21 +87,26 @@ __host__ __device__ inline nmc_sweep_layout nmc_sweep_lds(int nacc, int P, int p
 // Out-of-line helpers: the variate draws and the none/complete-pooling priors run once per
 // step on one wave; kept out of the step loop's body so their many polynomial constants are
 // materialized where they are used rather than hoisted into registers for the whole launch.
-// {z, log u} of step (it, p) of group g, chain c (nmc_step_variate: nmc_k_fill's values).
-__device__ __noinline__ nmc_d2 nmc_sweep_step_variate(const double* rz, const double* ru,
+// Part j of the variates of step (it, p) of group g, chain c, nmc_step_variate's values
+// split three ways so three waves draw them side by side (each ~1/3 of the ~460 VALU
+// instructions): j = 0 the Box-Muller radius sqrt(-2 log(1 - ua)), j = 1 its cosine
+// cos(2 pi ub) -- the normal is their product, rounded exactly as nmc_box_muller rounds it --
+// and j = 2 log u of the accept uniform.  Replay: the reference's z, 1.0 and log u.
+__device__ __noinline__ double nmc_sweep_variate_part(const double* rz, const double* ru,
                                                       int replay_n, int rng_mode, int P, int G,
                                                       int C, uint32_t ch, uint32_t seed, int it,
-                                                      int p, int g, int c) {
-  nmc_d2 r;
+                                                      int p, int g, int c, int j) {
   if (rng_mode == NMC_RNG_MODE_REPLAY) {
     const size_t k = (((size_t)it * P + p) * G + g) * C + c;
-    r.a = it < replay_n ? rz[k] : nmc_nan();
-    r.b = it < replay_n ? log(ru[k]) : nmc_nan();
-  } else {
-    r.a = nmc_normal(it, g, p, NMC_PURPOSE_PROPOSAL, ch, seed);
-    r.b = log(nmc_uniform2(it, g, p, NMC_PURPOSE_ACCEPT, ch, seed).a);
+    if (j == 1) return 1.0;
+    if (!(it < replay_n)) return nmc_nan();
+    return j == 0 ? rz[k] : log(ru[k]);
   }
-  return r;
+  const nmc_d2 u = nmc_uniform2(it, g, p, j == 2 ? NMC_PURPOSE_ACCEPT : NMC_PURPOSE_PROPOSAL,
+                                ch, seed);
+  if (j == 0) return sqrt(-2.0 * log(1.0 - u.a));
+  if (j == 1) return cos(6.283185307179586 * u.b);
+  return log(u.a);
 }
 // {hyper z, Gamma(a) draw} of the Gibbs update of parameter q after iteration t for chain c
 // (nmc_k_fill's values: Philox normal and Marsaglia-Tsang, or the replayed reference draws
@@ -246,20 +255,27 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
     return PARTIAL && !OWN && k0 + g < v.ge ? k0 + g : -1;
   };
   // {z, log u} of step (tn, pn) -> LDS slot `slot` (this lane's chain)
-  // d.zin: drawn here; otherwise the LDS-DMA of the pair nmc_k_fill wrote to the ring vzl
-  // (the issuing wave drains its vmcnt before the next barrier)
-  auto put_variates = [&](const View& v, int tn, int pn, int slot) {
+  // {z, log u} of step (tn, pn) -> LDS slot `slot`: part j of the draw (Dev.zin; j = 3: all
+  // three), or the LDS-DMA of the pair nmc_k_fill wrote to the ring vzl (the issuing wave
+  // drains its vmcnt before the next barrier; zm holds 1.0)
+  auto put_variates = [&](const View& v, int tn, int pn, int slot, int j) {
     if (d.zin) {
-      const nmc_d2 r = nmc_sweep_step_variate(d.rz, d.ru, d.replay_n, d.rng_mode, v.P, v.G, v.C,
-                                              (uint32_t)(d.chain_base + cc), d.seed, tn, pn, g,
-                                              cc);
-      lds[(v.L.zl + 2 * slot) * 64 + 2 * lane] = r.a;
-      lds[(v.L.zl + 2 * slot) * 64 + 2 * lane + 1] = r.b;
+      for (int jj = j == 3 ? 0 : j; jj <= (j == 3 ? 2 : j); ++jj) {
+        const double x = nmc_sweep_variate_part(d.rz, d.ru, d.replay_n, d.rng_mode, v.P, v.G,
+                                                v.C, (uint32_t)(d.chain_base + cc), d.seed, tn,
+                                                pn, g, cc, jj);
+        if (jj == 1) lds[(v.L.zm + slot) * 64 + lane] = x;
+        else lds[(v.L.zl + 2 * slot) * 64 + 2 * lane + (jj == 2 ? 1 : 0)] = x;
+      }
     } else {
       nmc_dma16(d.vzl + ((size_t)(tn - d.vbase) * v.P * v.G * v.C + (size_t)pn * v.G * v.C +
                          v.gc) * 2,
                 lds + (v.L.zl + 2 * slot) * 64);
     }
+  };
+  // this lane's proposal normal and log u of the step in slot sp
+  auto zval = [&](const nmc_sweep_layout& L, int sp) {
+    return lds[(L.zl + 2 * sp) * 64 + 2 * lane] * lds[(L.zm + sp) * 64 + lane];
   };
 
   NMC_RUN_SL(0);
@@ -304,7 +320,9 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
       }
     }
     if (ctl) {
-      put_variates(v, i0, 0, v.gs0 & 1);   // {z, log u} of the launch's first step
+      put_variates(v, i0, 0, v.gs0 & 1, 3);   // {z, log u} of the launch's first step
+      if (!d.zin)   // (the fill's ring holds z itself)
+        for (int k = 0; k < 2; ++k) lds[(L.zm + k) * 64 + lane] = 1.0;
       for (int j = 0; j < Fam::NACC; ++j)   // x + (-0.0) == x: the fixed slot sum
         for (int k = v.TI.nt; k < NMC_NSLOT; ++k)
           lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = -0.0;
@@ -372,8 +390,7 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         const double* hy = lds + L.hyp * 64 + lane;
         double* cwv = lds + L.cw * 64 + lane;
         const double x = th[p * 64];
-        const double prop = x + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
-                                    lds[(L.zl + 2 * sp) * 64 + 2 * lane];
+        const double prop = x + (1.0 * st[(NMC_ST_S * P + p) * 64]) * zval(L, sp);
         const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
         const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
         cwv[NMC_CW_LPC * 64] =
@@ -494,12 +511,12 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
             // overlaps everything below (d.zin: a queue job instead).  The slot held step
             // gs-1's pair, read by every wave before barrier B of gs-1.
           const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
-          if (tn < i1 && !d.zin) put_variates(v, tn, pn, sp ^ 1);
+          if (tn < i1 && !d.zin) put_variates(v, tn, pn, sp ^ 1, 3);
         }
         if (pend_p >= 0) apply_pending(v);
         c_v = th[p * 64];
         const double s = st[(NMC_ST_S * P + p) * 64];
-        c_prop = c_v + (1.0 * s) * lds[(L.zl + 2 * sp) * 64 + 2 * lane];   // propose (:304-306)
+        c_prop = c_v + (1.0 * s) * zval(L, sp);                              // propose (:304-306)
         c_lu = lds[(L.zl + 2 * sp) * 64 + 2 * lane + 1];
         {
           double thp[MP];
@@ -540,8 +557,7 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         double thp[MP];
 #pragma unroll
         for (int q = 0; q < MP; ++q) thp[q] = q < P ? th[q * 64] : 0.0;
-        const double prop = thp[p] + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
-                                         lds[(L.zl + 2 * sp) * 64 + 2 * lane];
+        const double prop = thp[p] + (1.0 * st[(NMC_ST_S * P + p) * 64]) * zval(L, sp);
 #pragma unroll
         for (int q = 0; q < MP; ++q)
           if (q == p) thp[q] = prop;
@@ -558,12 +574,27 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         }
         const double* lrows = lds + L.rows * 64;
         const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
-        const int zj = tn < i1 && d.zin ? 1 : 0;   // (the fill's ring: the control wave's DMA)
+        const int zj = tn < i1 && d.zin ? 3 : 0;   // (the fill's ring: the control wave's DMA)
         const int nt = v.TI.nt;
+        // the control wave arrives after its pre-work: it takes an entry only while the
+        // other queue waves have more than one round left (Dev.ctiles), so it never ends
+        // the step last; it looks before each take (no take in flight across a tile)
+        const bool cpick = ctl && d.ctiles != 2;
+        const int nother = W - 1 - (PARTIAL ? 1 : 0);
         auto grab = [&]() -> unsigned {
           unsigned k = 0;
-          if (lane == 0)
-            k = __hip_atomic_fetch_add(tcnt + sp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (lane == 0) {
+            if (cpick) {
+              k = __hip_atomic_load(tcnt + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              k = d.ctiles == 1 && (int)(nt + zj) - (int)k > nother
+                      ? __hip_atomic_fetch_add(tcnt + sp, 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP)
+                      : (unsigned)(nt + zj);
+            } else {
+              k = __hip_atomic_fetch_add(tcnt + sp, 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+          }
           return k;
         };
         int kq = (int)__builtin_amdgcn_readlane(grab(), 0);
@@ -571,9 +602,10 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         // has drained -- after this wave's first queue entry, not on the step's critical path
         bool pubdue = PARTIAL && ctl && pub_p >= 0;
         while (kq < nt + zj) {
-          const unsigned kn = grab();
+          const unsigned kn = cpick ? 0u : grab();
+          NMC_TILE_STAMP(kq, 0);
           if (kq < zj) {
-            put_variates(v, tn, pn, sp ^ 1);
+            put_variates(v, tn, pn, sp ^ 1, kq);
           } else {
             const int k = kq - zj;
             const int ra = v.TI.start(k), rn = v.TI.len(k);
@@ -587,11 +619,12 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
 #pragma unroll
             for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = acc[j];
           }
+          NMC_TILE_STAMP(kq, 1);
           if constexpr (PARTIAL) if (pubdue) {
             count_published();
             pubdue = false;
           }
-          kq = (int)__builtin_amdgcn_readlane(kn, 0);
+          kq = (int)__builtin_amdgcn_readlane(cpick ? grab() : kn, 0);
         }
         if constexpr (PARTIAL) if (pubdue) count_published();   // (no entry was left)
       }

@@ -221,7 +221,9 @@ class Engine:
         check(self.lib.nmc_split_config(self.h, ctypes.byref(sm), ctypes.byref(sb)))
         buf = ctypes.create_string_buffer(160)
         check(self.lib.nmc_kernel_name(self.h, buf, len(buf)))
+        zin = ctypes.c_int()
+        check(self.lib.nmc_variate_source(self.h, ctypes.byref(zin)))
         return dict(waves_per_group=w.value, chain_blocks=cb.value, persistent=bool(pe.value),
                     chains_per_block=cl.value, mode=MODE_NAMES.get(md.value, str(md.value)),
                     split_members=sm.value, chain_blocks_per_launch=sb.value,
-                    kernel=buf.value.decode())
+                    kernel=buf.value.decode(), zin=zin.value)

@@ -1,0 +1,66 @@
+"""bench.py's multi-rank arithmetic (N > 1 on CPU): every workload's per-rank chain blocks
+tile the job's chains exactly once, so value = job chains x groups x K / max-over-ranks
+time counts each (chain, group, iteration) once; the host bootstrap's max over two real
+processes is the slowest rank's time."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "mcmc-for-nested-data_amd"))
+
+import bench  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(bench.WORKLOADS))
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_rank_blocks_tile_the_job(name, world):
+    wl = dict(bench.WORKLOADS[name])
+    covered = []
+    for r in range(world):
+        c0, C = bench.rank_chains(wl, world, r)
+        assert C >= 1
+        covered.extend(range(c0, c0 + C))
+    assert covered == list(range(bench.job_chains(wl, world)))
+    if wl["scaling"] == "weak":   # fixed work per GPU
+        assert bench.job_chains(wl, world) == world * wl["chains"]
+    else:                         # fixed total work, blocks differ by at most one chain
+        sizes = [bench.rank_chains(wl, world, r)[1] for r in range(world)]
+        assert max(sizes) - min(sizes) <= 1 and sum(sizes) == wl["chains"]
+
+
+_WORKER = r"""
+import os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "mcmc-for-nested-data_amd"))
+from nestmc import parallel
+rank = int(os.environ["RANK"])
+hg = parallel.HostGroup(2, rank)
+t = parallel.max_over_ranks([0.25, 0.75][rank], hg)
+hg.barrier()
+hg.close()
+print("T=%r torch=%d" % (t, "torch" in sys.modules))
+"""
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_max_over_ranks_two_processes():
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), NMC_BOOTSTRAP_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", _WORKER, ROOT], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=60) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e
+        assert "T=0.75 torch=0" in o, (o, e)

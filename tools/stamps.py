@@ -59,7 +59,18 @@ def main():
                                                                numpy.median(cx, axis=0)]
                 res["blk0_w0"]["cw_poll_done"] = float(numpy.median(st[0, 0, 1:7, 8] -
                                                                 st[0, 0, 1:7, 0]))
-    print(json.dumps(dict(pooling=pooling, N=N, config=eng.launch_config(), stamps=res)))
+    # tile timeline of workgroup 0, steps 2..7 of the launch: [entry, wave, start, cycles],
+    # start relative to the step's first take
+    tw = numpy.frombuffer(out, dtype=numpy.uint64)[512:1024].reshape(8, 16, 4).astype(numpy.float64)
+    tiles = {}
+    for si in range(2, 8):
+        e = [(k, tw[si, k]) for k in range(16) if tw[si, k, 0] > 0 and tw[si, k, 1] > 0]
+        if not e:
+            continue
+        t0 = min(x[1][0] for x in e)
+        tiles["step%d" % si] = [[k, int(x[2]), int(x[0] - t0), int(x[1] - x[0])] for k, x in e]
+    print(json.dumps(dict(pooling=pooling, N=N, config=eng.launch_config(), stamps=res,
+                          tiles=tiles)))
     eng.close()
 
 
