@@ -173,6 +173,26 @@ struct Dev {
       if (e) d.stamps[512 + (si_ * 16 + (k)) * 4 + 2] = (unsigned long long)w;           \
     }                                                                                     \
   } while (0)
+// wave w of workgroup 0 arriving at barrier A of step si (< 8): stamps[512 + (si * 16 + w) * 4 + 3]
+#define NMC_ARRIVE_STAMP(si)                                                              \
+  do {                                                                                    \
+    if (d.stamps && blockIdx.x == 0 && (si) < 8 && w < 16 && lane == 0)                   \
+      d.stamps[512 + ((si) * 16 + w) * 4 + 3] = __builtin_amdgcn_s_memtime();              \
+  } while (0)
+// wave w of workgroup 0 at step si (< 8): stamps[1024 + 4 * 4096 + (si * 16 + w) * 4 + k],
+// k = 0 step top, 1 before the first take, 2 first take resolved
+#define NMC_RS_STAMP(si, k)                                                               \
+  do {                                                                                    \
+    if (d.stamps && blockIdx.x == 0 && (si) < 8 && w < 16 && lane == 0)                   \
+      d.stamps[1024 + 4 * 4096 + ((si) * 16 + w) * 4 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+// the control wave of workgroup 0 at step si: stamps[512 + (si * 16 + 12 + k) * 4 + 3],
+// k = 0 barrier A passed, 1 decided, 2 barrier B passed (W <= 12)
+#define NMC_CTL_STAMP(si, k)                                                              \
+  do {                                                                                    \
+    if (d.stamps && blockIdx.x == 0 && (si) < 8 && w == 0 && lane == 0)                   \
+      d.stamps[512 + ((si) * 16 + 12 + (k)) * 4 + 3] = __builtin_amdgcn_s_memtime();       \
+  } while (0)
 // every workgroup b: stamps[1024 + b * 4 + {entry, prologue done, loop done, exit}],
 // s_memrealtime (100 MHz, one clock for the whole chip; tools/launchtl.py)
 #define NMC_RUN_SL(slot)                                                                  \
@@ -183,6 +203,9 @@ struct Dev {
 #else
 #define NMC_RUN_SL(slot) do {} while (0)
 #define NMC_TILE_STAMP(k, e) do {} while (0)
+#define NMC_ARRIVE_STAMP(si) do {} while (0)
+#define NMC_RS_STAMP(si, k) do {} while (0)
+#define NMC_CTL_STAMP(si, k) do {} while (0)
 #define NMC_STAMP_CMP(t, slot) do {} while (0)
 #define NMC_STAMP_AUX(t, slot) do {} while (0)
 #define NMC_STAMP(t, slot) do {} while (0)
@@ -235,7 +258,7 @@ enum { NMC_RUN_HYPER_LOAD = 1 };
 enum { NMC_NSLOT = NMC_NSLOT_N };
 enum { NMC_SPIN_LIMIT = 1 << 22 };
 // diagnostic stamps buffer (make stamps): 1024 phase / tile words + 4 per workgroup
-enum { NMC_STAMP_WORDS = 1024 + 4 * 4096 };
+enum { NMC_STAMP_WORDS = 1024 + 4 * 4096 + 512 };
 // CU count the row split is sized for (a full MI355X), whatever the device reports
 enum { NMC_SPLIT_CU_BASIS = 256 };
 

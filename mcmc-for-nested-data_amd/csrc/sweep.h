@@ -61,15 +61,17 @@ struct nmc_sweep_layout {
               //                zl's z times zm (1.0 with the fill's ring; with Dev.zin the
               //                Box-Muller radius and cosine are two queue jobs)
   int cw;     // [8]            control values across the barriers (NMC_CW_*)
-  int flag;   // [1]            word 0 wait flag, words 1-2 Gibbs verdict by step parity,
-              //                uint32 words 8-9 the tile queues by step parity
+  int flag;   // [1]            column 0: word 0 wait flag, words 1-2 Gibbs verdict by step
+              //                parity, uint32 words 8-9 the tile queues by step parity,
+              //                uint32 words 32.. the step constants (NMC_SWK_AT)
   int rows;   // [nrows][NF]    the group's rows, staged once per launch
   int total;  // columns
 };
 __host__ __device__ inline nmc_sweep_layout nmc_sweep_lds(int nacc, int P, int partial,
                                                           int hlds, int G, int row_doubles) {
   nmc_sweep_layout L;
-  L.th = 0;
+  L.flag = 0;   // (first: its step constants, NMC_SWK_*, sit at a fixed address)
+  L.th = 1;
   L.part = L.th + P;
   L.st = L.part + nacc * NMC_NSLOT;
   L.hyp = L.st + 5 * P;
@@ -77,8 +79,7 @@ __host__ __device__ inline nmc_sweep_layout nmc_sweep_lds(int nacc, int P, int p
   L.zl = L.hval + (partial && hlds ? G + 1 : 0);
   L.zm = L.zl + 4;
   L.cw = L.zm + 2;
-  L.flag = L.cw + 8;
-  L.rows = L.flag + 1;
+  L.rows = L.cw + 8;
   // (+1 column: the pipelined likelihood loop prefetches one block past a wave's rows)
   L.total = L.rows + (row_doubles > 0 ? (row_doubles + 63) / 64 + 1 : 0);
   return L;
@@ -87,6 +88,16 @@ __host__ __device__ inline nmc_sweep_layout nmc_sweep_lds(int nacc, int P, int p
 // Out-of-line helpers: the variate draws and the none/complete-pooling priors run once per
 // step on one wave; kept out of the step loop's body so their many polynomial constants are
 // materialized where they are used rather than hoisted into registers for the whole launch.
+// The step constants: ints at word NMC_SWK_AT of LDS column 0 (the flag column), written
+// once by the prologue (after the column is zeroed) -- the problem
+// sizes, the group's row count and tiling and the carve's offsets -- so a step derives its
+// view with a few broadcast LDS reads at a fixed address (no kernel-argument or global load
+// on the step's critical path)
+enum { NMC_SWK_P = 0, NMC_SWK_G, NMC_SWK_C, NMC_SWK_NGRP, NMC_SWK_N, NMC_SWK_NT, NMC_SWK_H,
+       NMC_SWK_A, NMC_SWK_B, NMC_SWK_TH, NMC_SWK_PART, NMC_SWK_ST, NMC_SWK_HYP, NMC_SWK_HVAL,
+       NMC_SWK_ZL, NMC_SWK_ZM, NMC_SWK_CW, NMC_SWK_FLAG, NMC_SWK_ROWS, NMC_SWK_TOTAL,
+       NMC_SWK_COUNT = 20, NMC_SWK_AT = 32 };
+
 // Part j of the variates of step (it, p) of group g, chain c, nmc_step_variate's values
 // split three ways so three waves draw them side by side (each ~1/3 of the ~460 VALU
 // instructions): j = 0 the Box-Muller radius sqrt(-2 log(1 - ua)), j = 1 its cosine
@@ -231,15 +242,31 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
     nmc_sweep_layout L;
     nmc_tiling TI;
   };
-  auto view = [&]() {
+  // (pro: the prologue's view, from the group offsets in HBM; the steps read the group's
+  // row count and tiling from the LDS words the prologue stored, NMC_SWK_*)
+  auto view = [&](bool pro = false) {
     View v;
-    v.P = d.P; v.G = d.G; v.C = d.C;
+    if (pro) {
+      v.P = d.P; v.G = d.G; v.C = d.C;
+      v.ngrp = (int)(d.off[g + 1] - d.off[g]);
+      v.L = nmc_sweep_lds(Fam::NACC, v.P, PARTIAL, MODE == NMC_MODE_SYNC_LDS, v.G, d.nmax * NF);
+      v.TI = nmc_tiles(v.ngrp, d.tile);
+    } else {
+      int k[NMC_SWK_COUNT];
+      const int* kw = (const int*)lds + NMC_SWK_AT;
+#pragma unroll
+      for (int j = 0; j < NMC_SWK_COUNT; ++j) k[j] = __builtin_amdgcn_readfirstlane(kw[j]);
+      v.P = k[NMC_SWK_P]; v.G = k[NMC_SWK_G]; v.C = k[NMC_SWK_C]; v.ngrp = k[NMC_SWK_NGRP];
+      v.TI.n = k[NMC_SWK_N]; v.TI.nt = k[NMC_SWK_NT]; v.TI.h = k[NMC_SWK_H];
+      v.TI.a = k[NMC_SWK_A]; v.TI.b = k[NMC_SWK_B];
+      v.L.th = k[NMC_SWK_TH]; v.L.part = k[NMC_SWK_PART]; v.L.st = k[NMC_SWK_ST];
+      v.L.hyp = k[NMC_SWK_HYP]; v.L.hval = k[NMC_SWK_HVAL]; v.L.zl = k[NMC_SWK_ZL];
+      v.L.zm = k[NMC_SWK_ZM]; v.L.cw = k[NMC_SWK_CW]; v.L.flag = k[NMC_SWK_FLAG];
+      v.L.rows = k[NMC_SWK_ROWS]; v.L.total = k[NMC_SWK_TOTAL];
+    }
     v.lag = v.P >= 2 ? 2 : 1;                           // Gibbs task of step gs: gs - lag
     v.gs0 = i0 * v.P; v.ge = i1 * v.P;
-    v.ngrp = (int)(d.off[g + 1] - d.off[g]);
     v.gc = (size_t)g * v.C + cc;
-    v.L = nmc_sweep_lds(Fam::NACC, v.P, PARTIAL, MODE == NMC_MODE_SYNC_LDS, v.G, d.nmax * NF);
-    v.TI = nmc_tiles(v.ngrp, d.tile);
     return v;
   };
   auto hl_view = [](const nmc_sweep_layout& L) {   // the Gibbs helpers' view of the carve
@@ -282,7 +309,7 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
   // ---- prologue: the group's rows -> LDS (LDS-DMA, 1 KiB per wave-instruction), values and
   //      state -> LDS (parameter p by wave p % W) ----
   {
-    const View v = view();
+    const View v = view(true);
     const nmc_sweep_layout& L = v.L;
     double* lrows = lds + L.rows * 64;
     const int64_t ra0 = d.off[g];
@@ -326,7 +353,20 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
       for (int j = 0; j < Fam::NACC; ++j)   // x + (-0.0) == x: the fixed slot sum
         for (int k = v.TI.nt; k < NMC_NSLOT; ++k)
           lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = -0.0;
-      lds[L.flag * 64 + lane] = 0.0;       // (also zeroes the tile queues)
+      lds[L.flag * 64 + lane] = 0.0;
+      if (lane < 2)   // both tile queues: the first nq entries go by rank
+        ((unsigned*)(lds + L.flag * 64 + 4))[lane] = (unsigned)(W - 1 - (PARTIAL ? 1 : 0));
+      if (lane == 0) {                     // the step constants (view())
+        int* kw = (int*)lds + NMC_SWK_AT;
+        kw[NMC_SWK_P] = v.P; kw[NMC_SWK_G] = v.G; kw[NMC_SWK_C] = v.C;
+        kw[NMC_SWK_NGRP] = v.ngrp;
+        kw[NMC_SWK_N] = v.TI.n; kw[NMC_SWK_NT] = v.TI.nt; kw[NMC_SWK_H] = v.TI.h;
+        kw[NMC_SWK_A] = v.TI.a; kw[NMC_SWK_B] = v.TI.b;
+        kw[NMC_SWK_TH] = L.th; kw[NMC_SWK_PART] = L.part; kw[NMC_SWK_ST] = L.st;
+        kw[NMC_SWK_HYP] = L.hyp; kw[NMC_SWK_HVAL] = L.hval; kw[NMC_SWK_ZL] = L.zl;
+        kw[NMC_SWK_ZM] = L.zm; kw[NMC_SWK_CW] = L.cw; kw[NMC_SWK_FLAG] = L.flag;
+        kw[NMC_SWK_ROWS] = L.rows; kw[NMC_SWK_TOTAL] = L.total;
+      }
     }
     nmc_drain_vm();                        // this wave's row DMA has landed
   }
@@ -414,6 +454,7 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
                                r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        NMC_ARRIVE_STAMP((t - i0) * v.P + p);
         __syncthreads();   // A
         if (due) {
           ok = lds[v.L.flag * 64 + 1 + sp] == 2.0 * ((double)gs + 1);
@@ -488,9 +529,14 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
   for (int t = i0; t < i1 && ok; ++t) {
     NMC_STAMP(t, 0);
     for (int p = 0; p < d.P; ++p) {
+      NMC_RS_STAMP((t - i0) * d.P + p, 0);
       A = nmc_sweep_args_at<Fam>();
       const View v = view();
       const int P = v.P, G = v.G, C = v.C;
+#ifdef NMC_STAMPS
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      NMC_RS_STAMP((t - i0) * P + p, 1);
+#endif
       const nmc_sweep_layout& L = v.L;
       double* th = lds + L.th * 64 + lane;
       double* st = lds + L.st * 64 + lane;
@@ -576,33 +622,42 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
         const int zj = tn < i1 && d.zin ? 3 : 0;   // (the fill's ring: the control wave's DMA)
         const int nt = v.TI.nt;
-        // the control wave arrives after its pre-work: it takes an entry only while the
-        // other queue waves have more than one round left (Dev.ctiles), so it never ends
-        // the step last; it looks before each take (no take in flight across a tile)
-        const bool cpick = ctl && d.ctiles != 2;
-        const int nother = W - 1 - (PARTIAL ? 1 : 0);
-        auto grab = [&]() -> unsigned {
-          unsigned k = 0;
-          if (lane == 0) {
-            if (cpick) {
-              k = __hip_atomic_load(tcnt + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              k = d.ctiles == 1 && (int)(nt + zj) - (int)k > nother
-                      ? __hip_atomic_fetch_add(tcnt + sp, 1u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP)
-                      : (unsigned)(nt + zj);
-            } else {
-              k = __hip_atomic_fetch_add(tcnt + sp, 1u, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-          }
-          return k;
+        // The step's entries [0, ne): the zj variate jobs, then the nt tiles, in one LDS
+        // queue.  The nq queue waves (all but the control and the Gibbs wave) start on
+        // entries 0 .. nq-1 by rank, without a take (the counter starts at nq); further
+        // entries go to whichever wave asks first, the next take in flight during the entry.
+        // The control wave arrives after its pre-work and takes only while the others have
+        // more than a round left (Dev.ctiles), so it never ends the step last.  Entry ->
+        // partial slot is fixed: the sums stay in order.
+        const int ne = nt + zj;
+        unsigned* qc = tcnt + sp;
+        const int nq = W - 1 - (PARTIAL ? 1 : 0);
+        auto issue = [&]() -> unsigned {   // lane 0: a take
+          return lane == 0 ? __hip_atomic_fetch_add(qc, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP)
+                           : 0u;
         };
-        int kq = (int)__builtin_amdgcn_readlane(grab(), 0);
+        auto resolve = [&](unsigned i) -> int {   // the entry, -1: the queue is empty
+          const int e = (int)__builtin_amdgcn_readlane(i, 0);
+          return e < ne ? e : -1;
+        };
+        const bool cpick = ctl && d.ctiles != 2;
+        auto ctake = [&]() -> int {   // control: only while the others have a round left
+          if (d.ctiles != 1) return -1;
+          const unsigned i = lane == 0 ? __hip_atomic_load(qc, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP)
+                                       : 0u;
+          return ne - (int)__builtin_amdgcn_readlane(i, 0) > nq ? resolve(issue()) : -1;
+        };
+        const int rank = w - 1 - (PARTIAL ? 1 : 0);   // (control: -1)
+        NMC_RS_STAMP((t - i0) * P + p, 2);
+        int kq = cpick ? ctake() : ctl ? resolve(issue()) : (rank < ne ? rank : -1);
+        NMC_RS_STAMP((t - i0) * P + p, 3);
         // control: the count of the previous step's published value waits until its store
         // has drained -- after this wave's first queue entry, not on the step's critical path
         bool pubdue = PARTIAL && ctl && pub_p >= 0;
-        while (kq < nt + zj) {
-          const unsigned kn = cpick ? 0u : grab();
+        while (kq >= 0) {
+          const unsigned kn = cpick ? 0u : issue();
           NMC_TILE_STAMP(kq, 0);
           if (kq < zj) {
             put_variates(v, tn, pn, sp ^ 1, kq);
@@ -624,7 +679,7 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
             count_published();
             pubdue = false;
           }
-          kq = (int)__builtin_amdgcn_readlane(cpick ? grab() : kn, 0);
+          kq = cpick ? ctake() : resolve(kn);
         }
         if constexpr (PARTIAL) if (pubdue) count_published();   // (no entry was left)
       }
@@ -632,8 +687,20 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
       if (ctl) nmc_drain_vm();   // (its variate DMA has landed)
       if (p == 0) NMC_STAMP(t, 10);
       NMC_STAMP(t, 1 + 3 * (p & 1));
+      NMC_ARRIVE_STAMP((t - i0) * P + p);
       __syncthreads();   // A: every tile partial, the next step's variates, the Gibbs priors
       NMC_STAMP(t, 2 + 3 * (p & 1));
+      NMC_CTL_STAMP((t - i0) * P + p, 0);
+      {   // the view re-derived after the tile loop (nothing of it stays live across the loop)
+      A = nmc_sweep_args_at<Fam>();
+      const View v = view();
+      const nmc_sweep_layout& L = v.L;
+      double* th = lds + L.th * 64 + lane;
+      double* st = lds + L.st * 64 + lane;
+      double* cwv = lds + L.cw * 64 + lane;
+      unsigned* tcnt = (unsigned*)(lds + L.flag * 64 + 4);
+      const Fam& fam = A->fam;
+      const int G = v.G, C = v.C;
 
       // (partial pooling: the Gibbs wave's verdict is read in the same batch as the operands
       // and checked after the decision; an aborted step's decision is never used)
@@ -641,7 +708,9 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
       // ---- control: group log-likelihood of the proposal (tiles in order) and the
       //      Metropolis decision, one chain per lane (:334-383) ----
       if (ctl) {
-        if (lane == 0) tcnt[sp] = 0u;   // every entry is taken; the queue is reused at step +2
+        // every entry is taken; the queue is reused at step gs + 2 (its first nq entries
+        // by rank)
+        if (lane == 0) tcnt[sp] = (unsigned)(W - 1 - (PARTIAL ? 1 : 0));
         double acc[Fam::NACC];
 #pragma unroll
         for (int j = 0; j < Fam::NACC; ++j)
@@ -679,8 +748,11 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         ok = verdict == 2.0 * ((double)gs + 1);
         if (!ok) break;
       }
+      }
       if (p == 0) NMC_STAMP(t, 3);
+      NMC_CTL_STAMP((t - i0) * P + p, 1);
       __syncthreads();   // B: the decided value is visible to every wave
+      NMC_CTL_STAMP((t - i0) * P + p, 2);
     }
     NMC_STAMP(t, 6);
   }

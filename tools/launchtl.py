@@ -24,7 +24,7 @@ os.environ.setdefault("NESTMC_LIB", os.path.join(ROOT, "mcmc-for-nested-data_amd
                                                  "libnestmc_stamps.so"))
 import numpy  # noqa: E402
 
-WORDS = 1024 + 4 * 4096
+WORDS = 1024 + 4 * 4096 + 512
 
 
 def main():

@@ -36,7 +36,7 @@ def main():
     eng.synchronize()
     eng.lib.nmc_debug_stamps(eng.h, 1, None)
     eng.run(100, 120)
-    out = (ctypes.c_uint64 * (1024 + 4 * 4096))()   # NMC_STAMP_WORDS
+    out = (ctypes.c_uint64 * (1024 + 4 * 4096 + 512))()   # NMC_STAMP_WORDS
     eng.lib.nmc_debug_stamps(eng.h, 0, out)
     st = numpy.frombuffer(out, dtype=numpy.uint64)[:512].reshape(2, 2, 8, 16).astype(numpy.float64)
     res = {}
@@ -69,6 +69,13 @@ def main():
             continue
         t0 = min(x[1][0] for x in e)
         tiles["step%d" % si] = [[k, int(x[2]), int(x[0] - t0), int(x[1] - x[0])] for k, x in e]
+        # each wave's arrival at barrier A, relative to the same origin
+        tiles["arrive%d" % si] = [[w, int(tw[si, w, 3] - t0)] for w in range(12) if tw[si, w, 3] > 0]
+        tiles["ctl%d" % si] = [int(tw[si, 12 + k, 3] - t0) for k in range(3)]   # A, decided, B
+        tiles["t0_%d" % si] = int(t0)
+        rs = numpy.frombuffer(out, dtype=numpy.uint64)[17408:17920].reshape(8, 16, 4).astype(numpy.float64)
+        tiles["restart%d" % si] = [[w] + [int(rs[si, w, k] - t0) for k in range(4)]
+                                   for w in range(12) if rs[si, w, 0] > 0]
     print(json.dumps(dict(pooling=pooling, N=N, config=eng.launch_config(), stamps=res,
                           tiles=tiles)))
     eng.close()

@@ -26,7 +26,7 @@ import numpy  # noqa: E402
 
 from kbench import engine_for  # noqa: E402
 
-WORDS = 1024 + 4 * 4096
+WORDS = 1024 + 4 * 4096 + 512
 
 
 def main():

@@ -25,7 +25,7 @@ def main():
     eng.synchronize()
     eng.lib.nmc_debug_stamps(eng.h, 1, None)
     eng.run(100, 120)
-    out = (ctypes.c_uint64 * (1024 + 4 * 4096))()   # NMC_STAMP_WORDS
+    out = (ctypes.c_uint64 * (1024 + 4 * 4096 + 512))()   # NMC_STAMP_WORDS
     eng.lib.nmc_debug_stamps(eng.h, 0, out)
     st = numpy.frombuffer(out, dtype=numpy.uint64).astype(numpy.float64)
     ph = st[:512].reshape(2, 2, 8, 16)
