@@ -104,6 +104,8 @@ struct Dev {
   int ctiles;            // nmc_k_sweep, the control wave in the tile queue (NMC_CTL_TILES):
                          // 0 never, 1 only while the other waves have more than a round of
                          // entries left (default), 2 like every other wave
+  int gtiles;            // nmc_k_sweep, the Gibbs wave after its task (NMC_GIBBS_TILES): 0 no
+                         // tiles, 1 as ctiles 1 (default)
   int rows_lds;          // 1: each workgroup stages its group's rows in LDS once per launch
   int tile;              // target rows per likelihood tile (nmc_tiles)
   unsigned* cnt;         // [CB][P][32] publish counters (persistent partial): zeroed at create,

@@ -89,6 +89,7 @@ static void choose_geometry(nmc_ctx* x) {
   // leaf) and one parameter's chain-block values in LDS
   d.noprio = getenv("NMC_NOPRIO") ? atoi(getenv("NMC_NOPRIO")) : 0;   // diagnostics bits
   d.ctiles = getenv("NMC_CTL_TILES") ? atoi(getenv("NMC_CTL_TILES")) : 1;   // (Dev.ctiles)
+  d.gtiles = getenv("NMC_GIBBS_TILES") ? atoi(getenv("NMC_GIBBS_TILES")) : 1;   // (Dev.gtiles)
   d.hlds = d.naux > 0 && d.G <= 128 && lds_bytes_for(x, 1, d.rows_lds) <= (size_t)160 * 1024 &&
            !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
   // G <= 64: the Gibbs wave fetches a task's values into registers (one sc1 round trip)

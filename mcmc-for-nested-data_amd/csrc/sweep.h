@@ -98,6 +98,17 @@ enum { NMC_SWK_P = 0, NMC_SWK_G, NMC_SWK_C, NMC_SWK_NGRP, NMC_SWK_N, NMC_SWK_NT,
        NMC_SWK_ZL, NMC_SWK_ZM, NMC_SWK_CW, NMC_SWK_FLAG, NMC_SWK_ROWS, NMC_SWK_TOTAL,
        NMC_SWK_COUNT = 20, NMC_SWK_AT = 32 };
 
+// The step loop's workgroup barrier: LDS traffic only.  __syncthreads() is a workgroup-scope
+// release/acquire, which waits for every outstanding global store of the wave (vmcnt(0)):
+// the control wave's write-through publish and sample stores, the Gibbs wave's hyper-state
+// stores would then sit on the step's critical path.  The step loop shares nothing through
+// global memory inside the workgroup (a wave whose LDS-DMA must have landed drains vmcnt
+// itself first), so the barrier waits for LDS operations only; the "memory" clobber keeps
+// the compiler from moving memory accesses across it.
+__device__ __forceinline__ void nmc_step_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Part j of the variates of step (it, p) of group g, chain c, nmc_step_variate's values
 // split three ways so three waves draw them side by side (each ~1/3 of the ~460 VALU
 // instructions): j = 0 the Box-Muller radius sqrt(-2 log(1 - ua)), j = 1 its cosine
@@ -373,6 +384,105 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
   __syncthreads();
   NMC_RUN_SL(1);
 
+  // ---- the likelihood of the proposal (:615-635), tile by tile from the step's LDS queue;
+  //      with Dev.zin its first entries draw the next step's variates.  role 0: a queue wave,
+  //      1: the control wave, 2: the Gibbs wave ----
+  auto run_tiles = [&](const View& v, int t, int p, int role, auto&& after_first) {
+    const int P = v.P;
+    const nmc_sweep_layout& L = v.L;
+    const double* th = lds + L.th * 64 + lane;
+    const double* st = lds + L.st * 64 + lane;
+    unsigned* tcnt = (unsigned*)(lds + L.flag * 64 + 4);   // tile queues by step parity
+    const Fam& fam = A->fam;
+    const int sp = (t * P + p) & 1;
+        double thp[MP];
+#pragma unroll
+        for (int q = 0; q < MP; ++q) thp[q] = q < P ? th[q * 64] : 0.0;
+        const double prop = thp[p] + (1.0 * st[(NMC_ST_S * P + p) * 64]) * zval(L, sp);
+#pragma unroll
+        for (int q = 0; q < MP; ++q)
+          if (q == p) thp[q] = prop;
+        const typename Fam::Reg reg = fam.prepare(thp);
+        typename Fam::Reg preg = reg;   // paired rows: the partner lane's (lane ^ 32) values
+        if constexpr (nmc_paired_rows_ok<Fam>() && !HALF) if (d.paired) {
+          const bool hi = lane >= 32;
+#pragma unroll
+          for (int q = 0; q < MP; ++q) {
+            const nmc_pair2 e = nmc_halves(thp[q]);
+            thp[q] = hi ? e.lo : e.hi;
+          }
+          preg = fam.prepare(thp);
+        }
+        const double* lrows = lds + L.rows * 64;
+        const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
+        const int zj = tn < i1 && d.zin ? 3 : 0;   // (the fill's ring: the control wave's DMA)
+        const int nt = v.TI.nt;
+        // The step's entries [0, ne): the zj variate jobs, then the nt tiles, in one LDS
+        // queue.  The nq queue waves (all but the control and the Gibbs wave) start on
+        // entries 0 .. nq-1 by rank, without a take (the counter starts at nq); further
+        // entries go to whichever wave asks first, the next take in flight during the entry.
+        // The control wave arrives after its pre-work and takes only while the others have
+        // more than a round left (Dev.ctiles), so it never ends the step last.  Entry ->
+        // partial slot is fixed: the sums stay in order.
+        const int ne = nt + zj;
+        unsigned* qc = tcnt + sp;
+        const int nq = W - 1 - (PARTIAL ? 1 : 0);
+        auto issue = [&]() -> unsigned {   // lane 0: a take
+          return lane == 0 ? __hip_atomic_fetch_add(qc, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP)
+                           : 0u;
+        };
+        auto resolve = [&](unsigned i) -> int {   // the entry, -1: the queue is empty
+          const int e = (int)__builtin_amdgcn_readlane(i, 0);
+          return e < ne ? e : -1;
+        };
+        // role 1: the control wave (Dev.ctiles), 2: the Gibbs wave (Dev.gtiles) -- both take
+        // only while the queue waves have more than a round left
+        const int pol = role == 1 ? d.ctiles : role == 2 ? d.gtiles : 2;
+        const bool cpick = role != 0 && pol != 2;
+        auto ctake = [&]() -> int {   // control: only while the others have a round left
+          if (pol != 1) return -1;
+          const unsigned i = lane == 0 ? __hip_atomic_load(qc, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP)
+                                       : 0u;
+          return ne - (int)__builtin_amdgcn_readlane(i, 0) > nq ? resolve(issue()) : -1;
+        };
+        const int rank = w - 1 - (PARTIAL ? 1 : 0);   // (control: -1)
+        NMC_RS_STAMP((t - i0) * P + p, 2);
+        int kq = cpick ? ctake() : role != 0 ? resolve(issue()) : (rank < ne ? rank : -1);
+        NMC_RS_STAMP((t - i0) * P + p, 3);
+        // after_first: once, after this wave's first queue entry (or with none) -- the
+        // control's count of the previous step's published value waits for its store there,
+        // off the step's critical path
+        bool first = true;
+        while (kq >= 0) {
+          const unsigned kn = cpick ? 0u : issue();
+          NMC_TILE_STAMP(kq, 0);
+          if (kq < zj) {
+            put_variates(v, tn, pn, sp ^ 1, kq);
+          } else {
+            const int k = kq - zj;
+            const int ra = v.TI.start(k), rn = v.TI.len(k);
+            double acc[Fam::NACC];
+            bool done = false;
+            if constexpr (nmc_paired_rows_ok<Fam>()) if (HALF || d.paired) {
+              nmc_ll_rows_lds<Fam, true, HALF>(fam, reg, lrows + (size_t)ra * NF, rn, acc, &preg);
+              done = true;
+            }
+            if (!done) nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * NF, rn, acc);
+#pragma unroll
+            for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = acc[j];
+          }
+          NMC_TILE_STAMP(kq, 1);
+          if (first) {
+            after_first();
+            first = false;
+          }
+          kq = cpick ? ctake() : resolve(kn);
+        }
+        if (first) after_first();   // (no entry was left)
+  };
+
   bool ok = true;
   // ---- the Gibbs wave: its own loop, meeting the others at both barriers of every step ----
   if constexpr (PARTIAL) if (gw) {
@@ -454,13 +564,15 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
                                r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        // then the step's tiles while the queue waves have more than a round left
+        if (d.gtiles) run_tiles(v, t, p, 2, []() {});
         NMC_ARRIVE_STAMP((t - i0) * v.P + p);
-        __syncthreads();   // A
+        nmc_step_barrier();   // A
         if (due) {
           ok = lds[v.L.flag * 64 + 1 + sp] == 2.0 * ((double)gs + 1);
           if (!ok) break;
         }
-        __syncthreads();   // B
+        nmc_step_barrier();   // B
       }
     }
     // closing: task close_k (the matching barrier of the other waves' nmc_wait_published)
@@ -599,96 +711,15 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
       if (p == 0) NMC_STAMP(t, 8);   // (control: its pre-work done)
       // ---- every wave: the likelihood of the proposal (:615-635), tile by tile from the
       //      step's LDS queue; entry 0 (when there is a next step) draws its variates ----
-      {
-        double thp[MP];
-#pragma unroll
-        for (int q = 0; q < MP; ++q) thp[q] = q < P ? th[q * 64] : 0.0;
-        const double prop = thp[p] + (1.0 * st[(NMC_ST_S * P + p) * 64]) * zval(L, sp);
-#pragma unroll
-        for (int q = 0; q < MP; ++q)
-          if (q == p) thp[q] = prop;
-        const typename Fam::Reg reg = fam.prepare(thp);
-        typename Fam::Reg preg = reg;   // paired rows: the partner lane's (lane ^ 32) values
-        if constexpr (nmc_paired_rows_ok<Fam>() && !HALF) if (d.paired) {
-          const bool hi = lane >= 32;
-#pragma unroll
-          for (int q = 0; q < MP; ++q) {
-            const nmc_pair2 e = nmc_halves(thp[q]);
-            thp[q] = hi ? e.lo : e.hi;
-          }
-          preg = fam.prepare(thp);
-        }
-        const double* lrows = lds + L.rows * 64;
-        const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
-        const int zj = tn < i1 && d.zin ? 3 : 0;   // (the fill's ring: the control wave's DMA)
-        const int nt = v.TI.nt;
-        // The step's entries [0, ne): the zj variate jobs, then the nt tiles, in one LDS
-        // queue.  The nq queue waves (all but the control and the Gibbs wave) start on
-        // entries 0 .. nq-1 by rank, without a take (the counter starts at nq); further
-        // entries go to whichever wave asks first, the next take in flight during the entry.
-        // The control wave arrives after its pre-work and takes only while the others have
-        // more than a round left (Dev.ctiles), so it never ends the step last.  Entry ->
-        // partial slot is fixed: the sums stay in order.
-        const int ne = nt + zj;
-        unsigned* qc = tcnt + sp;
-        const int nq = W - 1 - (PARTIAL ? 1 : 0);
-        auto issue = [&]() -> unsigned {   // lane 0: a take
-          return lane == 0 ? __hip_atomic_fetch_add(qc, 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_WORKGROUP)
-                           : 0u;
-        };
-        auto resolve = [&](unsigned i) -> int {   // the entry, -1: the queue is empty
-          const int e = (int)__builtin_amdgcn_readlane(i, 0);
-          return e < ne ? e : -1;
-        };
-        const bool cpick = ctl && d.ctiles != 2;
-        auto ctake = [&]() -> int {   // control: only while the others have a round left
-          if (d.ctiles != 1) return -1;
-          const unsigned i = lane == 0 ? __hip_atomic_load(qc, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_WORKGROUP)
-                                       : 0u;
-          return ne - (int)__builtin_amdgcn_readlane(i, 0) > nq ? resolve(issue()) : -1;
-        };
-        const int rank = w - 1 - (PARTIAL ? 1 : 0);   // (control: -1)
-        NMC_RS_STAMP((t - i0) * P + p, 2);
-        int kq = cpick ? ctake() : ctl ? resolve(issue()) : (rank < ne ? rank : -1);
-        NMC_RS_STAMP((t - i0) * P + p, 3);
-        // control: the count of the previous step's published value waits until its store
-        // has drained -- after this wave's first queue entry, not on the step's critical path
-        bool pubdue = PARTIAL && ctl && pub_p >= 0;
-        while (kq >= 0) {
-          const unsigned kn = cpick ? 0u : issue();
-          NMC_TILE_STAMP(kq, 0);
-          if (kq < zj) {
-            put_variates(v, tn, pn, sp ^ 1, kq);
-          } else {
-            const int k = kq - zj;
-            const int ra = v.TI.start(k), rn = v.TI.len(k);
-            double acc[Fam::NACC];
-            bool done = false;
-            if constexpr (nmc_paired_rows_ok<Fam>()) if (HALF || d.paired) {
-              nmc_ll_rows_lds<Fam, true, HALF>(fam, reg, lrows + (size_t)ra * NF, rn, acc, &preg);
-              done = true;
-            }
-            if (!done) nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * NF, rn, acc);
-#pragma unroll
-            for (int j = 0; j < Fam::NACC; ++j) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = acc[j];
-          }
-          NMC_TILE_STAMP(kq, 1);
-          if constexpr (PARTIAL) if (pubdue) {
-            count_published();
-            pubdue = false;
-          }
-          kq = cpick ? ctake() : resolve(kn);
-        }
-        if constexpr (PARTIAL) if (pubdue) count_published();   // (no entry was left)
-      }
+      run_tiles(v, t, p, ctl ? 1 : 0, [&]() {
+        if constexpr (PARTIAL) if (ctl) count_published();
+      });
       if (p == 0) NMC_STAMP(t, 9);
       if (ctl) nmc_drain_vm();   // (its variate DMA has landed)
       if (p == 0) NMC_STAMP(t, 10);
       NMC_STAMP(t, 1 + 3 * (p & 1));
       NMC_ARRIVE_STAMP((t - i0) * P + p);
-      __syncthreads();   // A: every tile partial, the next step's variates, the Gibbs priors
+      nmc_step_barrier();   // A: every tile partial, the next step's variates, the Gibbs priors
       NMC_STAMP(t, 2 + 3 * (p & 1));
       NMC_CTL_STAMP((t - i0) * P + p, 0);
       {   // the view re-derived after the tile loop (nothing of it stays live across the loop)
@@ -751,7 +782,7 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
       }
       if (p == 0) NMC_STAMP(t, 3);
       NMC_CTL_STAMP((t - i0) * P + p, 1);
-      __syncthreads();   // B: the decided value is visible to every wave
+      nmc_step_barrier();   // B: the decided value is visible to every wave
       NMC_CTL_STAMP((t - i0) * P + p, 2);
     }
     NMC_STAMP(t, 6);
