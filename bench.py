@@ -352,10 +352,23 @@ def measure_traffic(args):
 
 
 def fam_instance(kernel):
-    """'FamLinreg<2>' out of 'nmc_k_run<FamLinreg<2>, NMC_MODE_..., true>'."""
+    """'FamLinreg<2>' out of 'nmc_k_run<FamLinreg<2>, NMC_MODE_..., true>', 'FamUser' out of
+    'nmc_k_run<FamUser, NMC_MODE_SYNC, false>': the first template argument."""
     i = kernel.find("<")
-    j = kernel.find(">", i + 1)
-    return kernel[i + 1:j + 1] if i >= 0 and j > i else kernel
+    if i < 0:
+        return kernel
+    depth = 0
+    for j in range(i + 1, len(kernel)):
+        ch = kernel[j]
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            if depth == 0:
+                return kernel[i + 1:j].strip()
+            depth -= 1
+        elif ch == "," and depth == 0:
+            return kernel[i + 1:j].strip()
+    return kernel[i + 1:].strip()
 
 
 def main():

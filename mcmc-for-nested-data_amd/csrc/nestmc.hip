@@ -141,13 +141,15 @@ static void choose_geometry(nmc_ctx* x) {
     d.RB = (d.C + d.CL - 1) / d.CL;
   }
 
-  // nmc_k_sweep (sweep.h): rows in LDS, no row split, none/complete pooling or partial
-  // pooling over one numpy leaf (G <= 128); up to 12 waves per workgroup (three per SIMD,
-  // <= 168 VGPRs), fewer when the grid needs two or three workgroups per CU.  Bit-identical
-  // to nmc_k_run; NMC_SWEEP=0 keeps nmc_k_run (the tests compare them).
+  // nmc_k_sweep (sweep.h), opt-in (NMC_SWEEP=1): rows in LDS, no row split, none/complete
+  // pooling or partial pooling over one numpy leaf per Gibbs wave or the Gibbs workgroups;
+  // up to 12 waves per workgroup (three per SIMD, <= 168 VGPRs), fewer when the grid needs
+  // two or three workgroups per CU.  Bit-identical to nmc_k_run (the tests compare them);
+  // measured no faster than nmc_k_run on cfg 2 / 3 / 4 (profiles/r04m_*.json), so not
+  // the default.
   x->sweep = false;
   if (d.rows_lds && d.S == 1 && !x->step_ok && !x->no_sweep &&
-      !(getenv("NMC_SWEEP") && !atoi(getenv("NMC_SWEEP"))) &&
+      getenv("NMC_SWEEP") && atoi(getenv("NMC_SWEEP")) != 0 &&
       (x->pooling != NMC_POOL_PARTIAL || d.nleaf <= 4)) {
     // (a multiple of four waves: a workgroup's waves spread evenly over the four SIMDs, so
     // two or three 4-wave workgroups per CU are resident whenever the occupancy API says so)

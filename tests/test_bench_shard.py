@@ -64,3 +64,13 @@ def test_max_over_ranks_two_processes():
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, e
         assert "T=0.75 torch=0" in o, (o, e)
+
+
+@pytest.mark.parametrize("kernel,inst", [
+    ("nmc_k_run<FamLinreg<2>, NMC_MODE_SYNC_REG, true>", "FamLinreg<2>"),
+    ("nmc_k_sweep<FamGaussMean<3>, NMC_MODE_HALF>", "FamGaussMean<3>"),
+    ("nmc_k_run<FamUser, NMC_MODE_SYNC, false>", "FamUser"),
+])
+def test_family_instance_of_kernel_name(kernel, inst):
+    """The roofline's per-row instruction count is keyed by the step kernel's family."""
+    assert bench.fam_instance(kernel) == inst

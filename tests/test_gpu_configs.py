@@ -49,12 +49,13 @@ def test_cfg4_geometry_multileaf_gibbs(gpu_lib, G):
     # one chain block: G workgroups + P Gibbs workgroups, co-resident -> persistent
     # (nmc_k_sweep SYNC_OWN: each task computed once per chain block by its Gibbs
     # workgroup, multi-leaf plan, read by every likelihood workgroup)
-    one = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed)
+    one = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed, env={"NMC_SWEEP": "1"})
     assert one[3]["persistent"], one[3]
     assert one[3]["kernel"].startswith("nmc_k_sweep<"), one[3]
     assert one[3]["mode"] == "NMC_MODE_SYNC_OWN", one[3]
-    # nmc_k_run's all-wave update (every workgroup streams the G values after barrier A)
-    syn = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed, env={"NMC_SWEEP": "0"})
+    # nmc_k_run's all-wave update (every workgroup streams the G values after barrier A):
+    # the default
+    syn = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed)
     assert syn[3]["mode"] == "NMC_MODE_SYNC", syn[3]
     # nmc_k_run's opt-in owner hand-off (task k updated once per chain block by group k % G's
     # Gibbs wave, the others read its four results; measured slower, kept bit-identical)
@@ -72,7 +73,9 @@ def test_cfg4_geometry_multileaf_gibbs(gpu_lib, G):
     spl = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, launch_iters=3,
                      env={"NMC_HOWN": "1", "NMC_SWEEP": "0"})
     # the sweep kernel's Gibbs workgroups over launches of 3, 3 and 2 iterations
-    swl = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, launch_iters=3)
+    swl = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, launch_iters=3,
+                     env={"NMC_SWEEP": "1"})
+    assert swl[3]["kernel"].startswith("nmc_k_sweep<"), swl[3]
     for k in range(3):
         assert numpy.array_equal(one[k], two[k][:64], equal_nan=True), k
         assert numpy.array_equal(one[k], own[k], equal_nan=True), k

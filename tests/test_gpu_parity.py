@@ -194,11 +194,11 @@ def test_eval_group_ll_matches_oracle(gpu_lib):
 def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
     """The paired-chain row loop (each lane evaluates its row pair half for its own chain
     and for lane ^ 32's, kernels.h nmc_ll_rows_lds<Fam, true>) reproduces the one-chain
-    broadcast loop bit for bit: flags, proposal LLs and recorded rows; so do nmc_k_run
-    (NMC_SWEEP=0: eight waves, every variate from the fill kernel) against the default
-    nmc_k_sweep (variates from the fill kernel's ring), nmc_k_sweep drawing every variate
-    itself (NMC_ZIN=1: three queue jobs per step, no fill launch), a four-wave nmc_k_sweep,
-    and the opt-in one-barrier step kernel (step.h, where it applies)."""
+    broadcast loop bit for bit: flags, proposal LLs and recorded rows; so do the default
+    nmc_k_run (eight waves, every variate from the fill kernel), the opt-in nmc_k_sweep
+    (NMC_SWEEP=1, twelve waves, variates from the fill kernel's ring), nmc_k_sweep drawing
+    every variate itself (NMC_ZIN=1: three queue jobs per step, no fill launch), a four-wave
+    nmc_k_sweep, and the opt-in one-barrier step kernel (step.h, where it applies)."""
     from gpu_cases import run_engine
     fam, sizes, priors, pooling, names = synthetic(kind, C, G, N, ragged=ragged)
     P = fam.n_params
@@ -208,11 +208,11 @@ def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
             # none pooling on few workgroups runs the half layout (32 chains per workgroup,
             # lane pairs on the two row parities); this keeps 64 chains per workgroup
             "full": {"NMC_HALF": "0"},
-            # nmc_k_run (eight waves, variates from the fill kernel) instead of nmc_k_sweep
-            "run": {"NMC_SWEEP": "0"},
+            # the opt-in nmc_k_sweep (twelve waves, variates from the fill kernel's ring)
+            "sweep": {"NMC_SWEEP": "1"},
             # nmc_k_sweep drawing its variates in the kernel; and on four waves
-            "zin": {"NMC_ZIN": "1"},
-            "sw4": {"NMC_SWEEP_WAVES": "4", "NMC_ZIN": "1"},
+            "zin": {"NMC_SWEEP": "1", "NMC_ZIN": "1"},
+            "sw4": {"NMC_SWEEP": "1", "NMC_SWEEP_WAVES": "4", "NMC_ZIN": "1"},
             # the opt-in one-barrier step kernel (step.h), both variant flags
             "step": {"NMC_STEP": "1", "NMC_STEP_FLAGS": "3"}}
     for name, env in envs.items():
@@ -221,8 +221,8 @@ def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
     if pooling != "partial":
         assert runs["paired"][3]["mode"] == "NMC_MODE_HALF", runs["paired"][3]
         assert runs["full"][3]["mode"] == "NMC_MODE_NOPOOL", runs["full"][3]
-    assert runs["paired"][3]["kernel"].startswith("nmc_k_sweep<"), runs["paired"][3]
-    assert runs["run"][3]["kernel"].startswith("nmc_k_run<"), runs["run"][3]
+    assert runs["paired"][3]["kernel"].startswith("nmc_k_run<"), runs["paired"][3]
+    assert runs["sweep"][3]["kernel"].startswith("nmc_k_sweep<"), runs["sweep"][3]
     for name in ("zin", "sw4"):
         assert runs[name][3]["kernel"].startswith("nmc_k_sweep<"), runs[name][3]
         assert runs[name][3]["zin"] == 1 and runs["paired"][3]["zin"] == 0, runs[name][3]
@@ -230,7 +230,7 @@ def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
         assert numpy.array_equal(runs["paired"][k], runs["bcast"][k], equal_nan=True), k
         assert numpy.array_equal(runs["paired"][k], runs["step"][k], equal_nan=True), k
         assert numpy.array_equal(runs["paired"][k], runs["full"][k], equal_nan=True), k
-        assert numpy.array_equal(runs["paired"][k], runs["run"][k], equal_nan=True), k
+        assert numpy.array_equal(runs["paired"][k], runs["sweep"][k], equal_nan=True), k
         assert numpy.array_equal(runs["paired"][k], runs["zin"][k], equal_nan=True), k
         assert numpy.array_equal(runs["paired"][k], runs["sw4"][k], equal_nan=True), k
     assert runs["paired"][0].mean() > 0.02
