@@ -1578,8 +1578,9 @@ enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
 typedef __attribute__((address_space(4))) const Dev* nmc_kdev_ptr;
 __device__ __forceinline__ const Dev* nmc_kdev() {
   nmc_kdev_ptr p = (nmc_kdev_ptr)__builtin_amdgcn_kernarg_segment_ptr();
-#ifndef NMC_STAMPS   // (the stamps build's divergent stamp stores make the backend move the
-                     //  laundered pointer to VGPRs, an illegal copy: diagnostics keep it plain)
+#if !defined(NMC_STAMPS) && !defined(NMC_NO_LAUNDER)
+  // (the stamps build's divergent stamp stores make the backend move the laundered pointer
+  //  to VGPRs, an illegal copy: diagnostics keep it plain; NMC_NO_LAUNDER: the A/B build)
   asm volatile("" : "+s"(p));
 #endif
   return (const Dev*)p;

@@ -32,6 +32,8 @@ def main():
             r = run("gauss", 256, 32, 500, "none", 0, 200)
         elif w == "cfg4":
             r = run("linreg", 128, 256, 2000, "partial", 0, 40)
+        elif w == "cfg4c64":   # one chain block of the cfg-4 geometry (half a shard)
+            r = run("linreg", 64, 256, 2000, "partial", 0, 40)
         elif w == "cfg4w4":   # four waves per workgroup: two workgroups per CU, resident
             r = run("linreg", 128, 256, 2000, "partial", 4, 40)
         elif w == "cfg5":

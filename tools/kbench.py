@@ -85,7 +85,7 @@ def run(kind, C, G, N, pooling, waves, iters, persist=None):
                 us_per_iter=ms * 1e3 / iters, wall_us_per_iter=wall * 1e6 / iters,
                 step_us_per_iter=kt["step_ms"] * 1e3 / max(1, kt["step_iters"]),
                 hyper_us=kt["hyper_ms"] * 1e3 / max(1, kt["hyper_launches"]),
-                rate=rate)
+                rate=rate, kernel=cfg["kernel"], mode=cfg["mode"])
 
 
 def main():
