@@ -259,14 +259,20 @@ def cpu_baseline(wl, window_s):
     t_start = min(s for s, _ in spans)
     t_end = max(e for _, e in spans)
     wall = t_end - t_start
-    rate = cores * wl["groups"] * iters / wall
+    # each process's own loop rate, summed: what the cores sustain together, without the
+    # start skew of the fork pool or one straggler on a shared host stretching the window
+    per = sorted(wl["groups"] * iters / (e - s) for s, e in spans)
+    rate = sum(per)
     out = {"value": rate, "unit": "chain*group*iter/s", "cores": cores, "kind": "port",
            "sample": "%d chains x %d iterations of the %s workload (%d groups x %d obs, %s "
                      "pooling) in the numpy oracle, one process per chain on %d cores (affinity "
-                     "mask %d); timed loop only (init excluded): %.1f s"
+                     "mask %d); timed loop only (init excluded), each process's loop rate "
+                     "summed; %.1f s from the first start to the last end"
                      % (cores, iters, wl.get("name", "?"), wl["groups"], wl["obs"],
                         wl["pooling"], cores, affinity, wall),
-           "timed_seconds": wall, "iterations": iters}
+           "timed_seconds": wall, "iterations": iters,
+           "value_wall": cores * wl["groups"] * iters / wall,
+           "per_process_min_max": [per[0], per[-1]]}
     cal = os.path.join(ROOT, "profiles", "cpu_calibration_r03.json")
     if wl.get("name") == "cfg3" and os.path.exists(cal):
         # the reference cannot travel to this box: its speed relative to the restatement
