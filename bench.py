@@ -340,7 +340,8 @@ def measure_traffic(args):
                     for row in csv.DictReader(fh):
                         kn = row.get("Kernel_Name", "")
                         if row.get("Counter_Name") == counter and \
-                                ("nmc_k_run" in kn or "nmc_k_sweep" in kn):
+                                ("nmc_k_run" in kn or "nmc_k_sweep" in kn) and \
+                                "nmc_k_sweep_gibbs" not in kn:
                             rows.append((int(row.get("Dispatch_Id", 0)),
                                          float(row["Counter_Value"])))
             if len(rows) < 2:

@@ -31,6 +31,8 @@ int nmc_fail(int code, const std::string& msg);
 struct nmc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t gstream = nullptr;          // nmc_k_sweep_gibbs beside the sweep (Dev.gsep)
+  hipEvent_t gev[2] = {nullptr, nullptr}; // fork / join of the two streams
   int C = 0, chain_base = 0, G = 0, P = 0, pooling = 0, family = 0, nf = 0, rng = 0;
   uint32_t seed = 0;
   int64_t n_obs = 0;
@@ -57,6 +59,7 @@ struct nmc_ctx {
   int* gidx = nullptr;                    // [n_obs] group of each observation (obs-LL rows)
   int64_t nmax_group = 0;                 // rows of the largest group
   int split_batch = 0;                    // row split: chain blocks per (resident) launch
+  int sweep_batch = 0;                    // nmc_k_sweep with Dev.gsep: chain blocks per launch
   volatile unsigned* tmo_host = nullptr;  // host view of d.tmo (coherent pinned memory)
   void* user = nullptr;                   // user family: its per-device kernel table (user.hip)
   double* user_k = nullptr;               // user family: device copy of the model constants
@@ -105,14 +108,20 @@ static inline size_t sweep_lds_bytes(const nmc_ctx* x) {
   const bool partial = x->pooling == NMC_POOL_PARTIAL;
   size_t b = (size_t)nmc_sweep_lds(x->nacc, d.P, partial, d.G > 64 && d.G <= 128 ? 1 : 0, d.G,
                                    d.nmax * x->nf).total * 512;
-  if (partial && d.G > 128)
+  if (partial && d.G > 128 && !d.gsep)
     b = std::max(b, (size_t)nmc_lds(0, d.P, 1, d.nleaf, d.ntail, d.W, d.G, 0, 0).total * 512);
   return b;
+}
+// dynamic LDS of nmc_k_sweep_gibbs (four waves)
+static inline size_t sweep_gibbs_lds_bytes(const nmc_ctx* x) {
+  const Dev& d = x->d;
+  return (size_t)nmc_lds(0, d.P, 1, d.nleaf, d.ntail, 4, d.G, 0, 0).total * 512;
 }
 // workgroups of the sweep grid: RB * G likelihood workgroups (+ RB * P Gibbs workgroups)
 static inline int64_t sweep_grid(const nmc_ctx* x) {
   const Dev& d = x->d;
-  return (int64_t)d.RB * d.G + (x->pooling == NMC_POOL_PARTIAL && d.G > 128 ? (int64_t)d.RB * d.P : 0);
+  return (int64_t)d.RB * d.G +
+         (x->pooling == NMC_POOL_PARTIAL && d.G > 128 && !d.gsep ? (int64_t)d.RB * d.P : 0);
 }
 
 static inline size_t run_lds_bytes(const nmc_ctx* x) {
@@ -178,11 +187,16 @@ static int nmc_run_launches(nmc_ctx* x, int i0, int i1, Launch&& launch) {
   }
   const dim3 block(64 * d.W);
   const int mode = run_mode(x);
-  if (d.S > 1) {   // row split: resident batches of chain blocks
-    for (int cb0 = 0; cb0 < d.RB; cb0 += x->split_batch) {
+  const bool batched = d.S > 1 || (x->sweep && d.gsep && x->sweep_batch > 0 &&
+                                   x->sweep_batch < d.RB);
+  const int batch = d.S > 1 ? x->split_batch : x->sweep_batch;
+  if (batched) {
+    // resident batches of chain blocks (chain blocks are independent): the row split, and
+    // the sweep with its Gibbs kernel when the whole grid is not co-resident
+    for (int cb0 = 0; cb0 < d.RB; cb0 += batch) {
       Dev db = d;
       db.cb0 = cb0;
-      const int nb = std::min(x->split_batch, d.RB - cb0);
+      const int nb = std::min(batch, d.RB - cb0);
       launch(mode, db, dim3(nb * d.G * d.S), block, lds);
     }
   } else {

@@ -148,8 +148,16 @@ static void choose_geometry(nmc_ctx* x) {
   // measured no faster than nmc_k_run on cfg 2 / 3 / 4 (profiles/r04m_*.json), so not
   // the default.
   x->sweep = false;
-  if (d.rows_lds && d.S == 1 && !x->step_ok && !x->no_sweep &&
-      getenv("NMC_SWEEP") && atoi(getenv("NMC_SWEEP")) != 0 &&
+  d.gsep = 0;
+  // default: partial pooling over more than one Gibbs leaf (G > 128, cfg 4), where the
+  // Gibbs workgroups (SYNC_OWN) take the update off the critical path: 33.8 against
+  // nmc_k_run's 52.1 us/iter at the cfg-4 shard (profiles/r04q_cfg4_gsep.jsonl);
+  // NMC_SWEEP=1 everywhere it applies, NMC_SWEEP=0 never
+  const char* sw_env = getenv("NMC_SWEEP");
+  const bool sweep_want = sw_env ? atoi(sw_env) != 0
+                                 : x->pooling == NMC_POOL_PARTIAL && d.G > 128 &&
+                                       x->family < NMC_LL_USER_BASE;
+  if (d.rows_lds && d.S == 1 && !x->step_ok && !x->no_sweep && sweep_want &&
       (x->pooling != NMC_POOL_PARTIAL || d.nleaf <= 4)) {
     // (a multiple of four waves: a workgroup's waves spread evenly over the four SIMDs, so
     // two or three 4-wave workgroups per CU are resident whenever the occupancy API says so)
@@ -161,10 +169,18 @@ static void choose_geometry(nmc_ctx* x) {
       if (v >= 3 && v <= NMC_SWEEP_THREADS / 64) sw = v;
     }
     // partial pooling: a control, a Gibbs and at least one likelihood wave, all resident
-    if (x->pooling != NMC_POOL_PARTIAL || wgs <= 3 * (int64_t)x->ncu) {
+    // (G > 128, built-in families: in resident batches of chain blocks if need be, with
+    // the Gibbs workgroups as their own kernel -- nmc_create)
+    if (x->pooling != NMC_POOL_PARTIAL || wgs <= 3 * (int64_t)x->ncu ||
+        (d.G > 128 && x->family < NMC_LL_USER_BASE)) {
       x->sweep = true;
       d.W = sw;
     }
+    // (SYNC_OWN's Gibbs workgroups go into their own kernel, Dev.gsep, only when the one
+    // grid cannot be resident: nmc_create; NMC_GSEP=1 forces it)
+    if (x->sweep && x->pooling == NMC_POOL_PARTIAL && d.G > 128 &&
+        x->family < NMC_LL_USER_BASE && getenv("NMC_GSEP"))
+      d.gsep = atoi(getenv("NMC_GSEP")) != 0;
   }
 }
 
@@ -281,6 +297,9 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   e = hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking);
   if (e != hipSuccess) { nmc_destroy(x); return fail(-2, std::string("hipStreamCreate: ") + hipGetErrorString(e)); }
   for (auto& ev : x->ev) hipEventCreate(&ev);
+  e = hipStreamCreateWithFlags(&x->gstream, hipStreamNonBlocking);
+  if (e != hipSuccess) { nmc_destroy(x); return fail(-2, std::string("hipStreamCreate: ") + hipGetErrorString(e)); }
+  for (auto& ev : x->gev) hipEventCreateWithFlags(&ev, hipEventDisableTiming);
 
   Dev& d = x->d;
   const size_t PGC = (size_t)n_params * n_groups * n_chains, GC = (size_t)n_groups * n_chains,
@@ -406,6 +425,13 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     NmcCall c;
     c.op = NMC_OP_CAN_PERSIST;
     if (int rc2 = nmc_call_family(x, c)) { nmc_destroy(x); return rc2; }
+    if (x->sweep && c.result != 1 && run_mode(x) == NMC_MODE_SYNC_OWN && !d.gsep &&
+        x->family < NMC_LL_USER_BASE && !getenv("NMC_GSEP")) {
+      // the likelihood and Gibbs workgroups in one grid do not fit: two kernels, one per
+      // stream (nmc_k_sweep + nmc_k_sweep_gibbs), each workgroup with its own LDS size
+      d.gsep = 1;
+      if (int rc2 = nmc_call_family(x, c)) { nmc_destroy(x); return rc2; }
+    }
     if (x->sweep && c.result != 1) {   // the sweep grid cannot be resident: nmc_k_run
       x->no_sweep = true;
       choose_geometry(x);
@@ -477,6 +503,9 @@ int nmc_destroy(nmc_ctx* x) {
   for (auto& ev : x->ev) if (ev) hipEventDestroy(ev);
   for (auto& pr : x->kev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   for (auto& pr : x->hev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+  if (x->gstream) hipStreamSynchronize(x->gstream);
+  for (auto& ev : x->gev) if (ev) hipEventDestroy(ev);
+  if (x->gstream) hipStreamDestroy(x->gstream);
   if (x->stream) hipStreamDestroy(x->stream);
   if (x->tmo_host) hipHostFree((void*)x->tmo_host);
   delete x;
@@ -845,7 +874,9 @@ int nmc_get_kernel_timing(nmc_ctx* x, double* step_ms, int64_t* step_n, int64_t*
 
 int nmc_split_config(nmc_ctx* x, int* members, int* chain_blocks_per_launch) {
   *members = x->d.S;
-  *chain_blocks_per_launch = x->d.S > 1 ? x->split_batch : x->d.RB;
+  *chain_blocks_per_launch = x->d.S > 1 ? x->split_batch
+                             : x->sweep && x->d.gsep && x->sweep_batch > 0 ? x->sweep_batch
+                                                                           : x->d.RB;
   return 0;
 }
 

@@ -168,6 +168,75 @@ __device__ __forceinline__ const nmc_sweep_args<Fam>* nmc_sweep_args_at() {
   return (const nmc_sweep_args<Fam>*)q;
 }
 
+// SYNC_OWN's Gibbs workgroup kb = (chain block, parameter q), four waves: every task (t, q)
+// of the launch in order, once its publication is complete -- HyperParameter.update
+// (:463-498) computed once per chain block, written through and counted ready (nmc_hrd)
+// for the likelihood workgroups' Gibbs waves.
+template <class Fam>
+__device__ __forceinline__ void nmc_sweep_gibbs_wg(int kb, double* lds) {
+  const nmc_sweep_args<Fam>* A = nmc_sweep_args_at<Fam>();
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int W = blockDim.x >> 6;
+  const int i0 = A->i0, i1 = A->i1;
+#define d (A->d)
+  const int P = d.P, G = d.G, C = d.C;
+  const int hcb = d.cb0 + kb / P, q = kb % P;
+  const int c = hcb * 64 + lane;
+  const int cc = c < C ? c : C - 1;
+  const nmc_lds_layout H = nmc_lds(0, P, 1, d.nleaf, d.ntail, W, G, 0, 0);
+  double* hy = lds + H.hyp * 64 + lane;
+  if (w == 0) {   // the state of q after iteration i0-1 (slot (i0-1) & 1)
+    const size_t ho = nmc_hslot(d, i0 - 1) + (size_t)q * C + cc;
+    hy[(NMC_HY_MU * P + q) * 64] = d.mu[ho];
+    hy[(NMC_HY_SD * P + q) * 64] = d.hsd[ho];
+    hy[(NMC_HY_LSD * P + q) * 64] = d.hlsd[ho];
+    hy[(NMC_HY_S2 * P + q) * 64] = d.s2[ho];
+  }
+  for (int t = i0; t < i1; ++t) {
+    A = nmc_sweep_args_at<Fam>();
+    if (!nmc_wait_published(d, hcb, q, (unsigned)d.G * (unsigned)(t - i0 + 1), lds, H)) break;
+    if (w == 0) {   // the task's variates and sqrt(s2 / G) of the previous update
+      nmc_d2 hv;
+      if (d.zin) {
+        hv = nmc_sweep_hyper_variate(d.rhz, d.rhu, d.replay_n, d.rng_mode, d.P, d.C,
+                                     (uint32_t)(d.chain_base + cc), d.seed, d.ha, d.hlga, t, q,
+                                     cc);
+      } else {
+        const size_t hvi = (((size_t)(t - d.vbase) * d.P + q) * d.C + cc) * 2;
+        hv.a = d.vh[hvi];
+        hv.b = d.vh[hvi + 1];
+      }
+      lds[H.hv * 64 + (q * 64 + lane) * 2] = hv.a;
+      lds[H.hv * 64 + (q * 64 + lane) * 2 + 1] = hv.b;
+      hy[(NMC_HY_SDM * d.P + q) * 64] = sqrt(hy[(NMC_HY_S2 * d.P + q) * 64] / d.G);
+    }
+    __syncthreads();
+    // HyperParameter.update (:463-498) for the chain block, written through to the global
+    // slot of t (and the sample row); wave 0 stored it and counts it ready
+    nmc_hyper<NMC_SRC_SC1, 4, true>(d, (t & 1) ? d.vb1 : d.vb0, hcb, t, lds, H, true, q);
+    if (w == 0) {
+      nmc_drain_vm();
+      if (lane == 0)
+        __hip_atomic_fetch_add(nmc_hrd(d, hcb, q), 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  nmc_drain_vm();
+#undef d
+}
+
+// Dev.gsep: the Gibbs workgroups of SYNC_OWN as a kernel of their own (RB * P workgroups
+// of four waves, the small nmc_lds carve), launched on a second stream beside
+// nmc_k_sweep's RB * G likelihood workgroups: co-resident with two 61-KB likelihood
+// workgroups per CU where one kernel with a single LDS size would not be.
+template <class Fam>
+__global__ void __launch_bounds__(256) nmc_k_sweep_gibbs(nmc_sweep_args<Fam> a_arg) {
+  (void)a_arg;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  nmc_sweep_gibbs_wg<Fam>((int)blockIdx.x, lds);
+}
+
 template <class Fam, int MODE>
 __global__ void __launch_bounds__(NMC_SWEEP_THREADS)
 nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
@@ -188,57 +257,15 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
   const int W = blockDim.x >> 6;
   const int i0 = A->i0, i1 = A->i1;
 
-  // ---- SYNC_OWN: the Gibbs workgroups (blocks RB * G ..), one per (chain block, parameter q):
-  //      every task (t, q) of the launch in order, once its publication is complete ----
-  if constexpr (OWN) if ((int)blockIdx.x >= d.RB * d.G) {
-    const int kb = (int)blockIdx.x - d.RB * d.G;
-    const int P = d.P, G = d.G, C = d.C;
-    const int hcb = kb / P, q = kb % P;
-    const int c = hcb * 64 + lane;
-    const int cc = c < C ? c : C - 1;
-    const nmc_lds_layout H = nmc_lds(0, P, 1, d.nleaf, d.ntail, W, G, 0, 0);
-    double* hy = lds + H.hyp * 64 + lane;
-    if (w == 0) {   // the state of q after iteration i0-1 (slot (i0-1) & 1)
-      const size_t ho = nmc_hslot(d, i0 - 1) + (size_t)q * C + cc;
-      hy[(NMC_HY_MU * P + q) * 64] = d.mu[ho];
-      hy[(NMC_HY_SD * P + q) * 64] = d.hsd[ho];
-      hy[(NMC_HY_LSD * P + q) * 64] = d.hlsd[ho];
-      hy[(NMC_HY_S2 * P + q) * 64] = d.s2[ho];
-    }
-    for (int t = i0; t < i1; ++t) {
-      A = nmc_sweep_args_at<Fam>();
-      if (!nmc_wait_published(d, hcb, q, (unsigned)d.G * (unsigned)(t - i0 + 1), lds, H)) break;
-      if (w == 0) {   // the task's variates and sqrt(s2 / G) of the previous update
-        nmc_d2 hv;
-        if (d.zin) {
-          hv = nmc_sweep_hyper_variate(d.rhz, d.rhu, d.replay_n, d.rng_mode, d.P, d.C,
-                                       (uint32_t)(d.chain_base + cc), d.seed, d.ha, d.hlga, t, q,
-                                       cc);
-        } else {
-          const size_t hvi = (((size_t)(t - d.vbase) * d.P + q) * d.C + cc) * 2;
-          hv.a = d.vh[hvi];
-          hv.b = d.vh[hvi + 1];
-        }
-        lds[H.hv * 64 + (q * 64 + lane) * 2] = hv.a;
-        lds[H.hv * 64 + (q * 64 + lane) * 2 + 1] = hv.b;
-        hy[(NMC_HY_SDM * d.P + q) * 64] = sqrt(hy[(NMC_HY_S2 * d.P + q) * 64] / d.G);
-      }
-      __syncthreads();
-      // HyperParameter.update (:463-498) for the chain block, written through to the global
-      // slot of t (and the sample row); wave 0 stored it and counts it ready
-      nmc_hyper<NMC_SRC_SC1, 4, true>(d, (t & 1) ? d.vb1 : d.vb0, hcb, t, lds, H, true, q);
-      if (w == 0) {
-        nmc_drain_vm();
-        if (lane == 0)
-          __hip_atomic_fetch_add(nmc_hrd(d, hcb, q), 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    nmc_drain_vm();
+  // ---- SYNC_OWN: the Gibbs workgroups (blocks RB * G .., unless Dev.gsep puts them in
+  //      their own kernel, nmc_k_sweep_gibbs) ----
+  if constexpr (OWN) if (!d.gsep && (int)blockIdx.x >= d.RB * d.G) {
+    nmc_sweep_gibbs_wg<Fam>((int)blockIdx.x - d.RB * d.G, lds);
     return;
   }
 
-  const int g = blockIdx.x % d.G, cb = blockIdx.x / d.G;
+  // (Dev.cb0: the first chain block of this launch -- resident batches of chain blocks)
+  const int g = blockIdx.x % d.G, cb = d.cb0 + (int)blockIdx.x / d.G;
   const int c = HALF ? cb * 32 + (lane & 31) : cb * 64 + lane;
   const bool live = c < d.C && (!HALF || lane < 32);   // writes this lane's outputs
   const int cc = c < d.C ? c : d.C - 1;

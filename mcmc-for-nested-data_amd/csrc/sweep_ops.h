@@ -33,6 +33,20 @@ static int nmc_sweep_call_t(nmc_ctx* x, const Fam& fam, NmcCall& c) {
                                              size_t lds) {
         nmc_sweep_args<Fam> a{d, fam, i0, i1};
         void* args[] = {&a};
+        if (mode == NMC_MODE_SYNC_OWN && d.gsep) {
+          // the Gibbs workgroups' kernel on the second stream, forked after the work before
+          // this launch and joined before the work after it; both kernels resident together
+          // (NMC_OP_CAN_PERSIST), each spinning only on counters the other advances
+          hipEventRecord(x->gev[0], x->stream);
+          hipStreamWaitEvent(x->gstream, x->gev[0], 0);
+          const unsigned nb = grid.x / (unsigned)d.G;   // chain blocks of this launch
+          hipLaunchKernel((const void*)nmc_k_sweep_gibbs<Fam>, dim3(nb * d.P), dim3(256), args,
+                          sweep_gibbs_lds_bytes(x), x->gstream);
+          hipLaunchKernel(nmc_sweep_kernel<Fam>(mode), grid, block, args, lds, x->stream);
+          hipEventRecord(x->gev[1], x->gstream);
+          hipStreamWaitEvent(x->stream, x->gev[1], 0);
+          return;
+        }
         // (SYNC_OWN: the Gibbs workgroups after the likelihood ones)
         const dim3 gr(mode == NMC_MODE_SYNC_OWN ? (unsigned)sweep_grid(x) : grid.x);
         hipLaunchKernel(nmc_sweep_kernel<Fam>(mode), gr, block, args, lds, x->stream);
@@ -49,6 +63,28 @@ static int nmc_sweep_call_t(nmc_ctx* x, const Fam& fam, NmcCall& c) {
       if (k && hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W,
                                                             nmc_persist_lds(x)) == hipSuccess)
         c.result = sweep_grid(x) <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
+      if (x->d.gsep && k) {
+        // the largest batch of chain blocks whose likelihood workgroups are co-resident and
+        // leave, on the CUs holding the most of them, the LDS and the wave slots (<= 168
+        // VGPRs: three waves per SIMD) for one four-wave Gibbs workgroup; the launches run
+        // the chain blocks in such batches (nmc_run_launches)
+        int ng = 0;
+        const bool gok = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                             &ng, (const void*)nmc_k_sweep_gibbs<Fam>, 256,
+                             sweep_gibbs_lds_bytes(x)) == hipSuccess && ng >= 1;
+        const int64_t cap = (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
+        int best = 0;
+        for (int b = 1; gok && b <= x->d.RB; ++b) {
+          const int64_t wg = (int64_t)b * x->d.G;
+          const int64_t per = (wg + x->ncu - 1) / x->ncu;
+          if (wg <= cap &&
+              per * (int64_t)nmc_persist_lds(x) + sweep_gibbs_lds_bytes(x) <= (size_t)160 * 1024 &&
+              per * x->d.W + 4 <= 12)
+            best = b;
+        }
+        x->sweep_batch = best;
+        c.result = best >= 1;
+      }
       return 0;
     }
     case NMC_OP_CAPACITY: {

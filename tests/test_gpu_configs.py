@@ -53,9 +53,8 @@ def test_cfg4_geometry_multileaf_gibbs(gpu_lib, G):
     assert one[3]["persistent"], one[3]
     assert one[3]["kernel"].startswith("nmc_k_sweep<"), one[3]
     assert one[3]["mode"] == "NMC_MODE_SYNC_OWN", one[3]
-    # nmc_k_run's all-wave update (every workgroup streams the G values after barrier A):
-    # the default
-    syn = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed)
+    # nmc_k_run's all-wave update (every workgroup streams the G values after barrier A)
+    syn = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed, env={"NMC_SWEEP": "0"})
     assert syn[3]["mode"] == "NMC_MODE_SYNC", syn[3]
     # nmc_k_run's opt-in owner hand-off (task k updated once per chain block by group k % G's
     # Gibbs wave, the others read its four results; measured slower, kept bit-identical)
@@ -65,7 +64,7 @@ def test_cfg4_geometry_multileaf_gibbs(gpu_lib, G):
     assert own[3]["kernel"].startswith("nmc_k_run<"), own[3]
     # the same chains in a two-block launch (two 4-wave workgroups per CU, persistent) and
     # forced launch per iteration
-    two = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed)
+    two = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, env={"NMC_SWEEP": "0"})
     lau = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, env={"NMC_PERSIST": "0"})
     assert not lau[3]["persistent"]
     # owner hand-off in launches of 3, 3 and 2 iterations (each launch's closing task,
@@ -77,7 +76,15 @@ def test_cfg4_geometry_multileaf_gibbs(gpu_lib, G):
     swl = run_engine(fam, sizes, st, numpy.arange(64), 0, n_iter, seed, launch_iters=3,
                      env={"NMC_SWEEP": "1"})
     assert swl[3]["kernel"].startswith("nmc_k_sweep<"), swl[3]
+    # two chain blocks on the sweep (the default for G > 128): at G = 256 the Gibbs
+    # workgroups run as their own kernel on a second stream (Dev.gsep), co-resident with the
+    # 512 likelihood workgroups
+    sep = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed)
+    if G == 256:
+        assert sep[3]["kernel"].startswith("nmc_k_sweep<"), sep[3]
+        assert sep[3]["mode"] == "NMC_MODE_SYNC_OWN", sep[3]
     for k in range(3):
+        assert numpy.array_equal(two[k], sep[k], equal_nan=True), k
         assert numpy.array_equal(one[k], two[k][:64], equal_nan=True), k
         assert numpy.array_equal(one[k], own[k], equal_nan=True), k
         assert numpy.array_equal(one[k], syn[k], equal_nan=True), k
