@@ -168,11 +168,134 @@ __device__ __forceinline__ const nmc_sweep_args<Fam>* nmc_sweep_args_at() {
   return (const nmc_sweep_args<Fam>*)q;
 }
 
+// HyperParameter.update (:463-498) of parameter q for one chain block, as nmc_hyper<SC1, NS,
+// true> (the same streams, sums and order, so the same bits) but loading the G values once:
+// each wave keeps its NS streams' values in registers for the second pass (sum of squares
+// about the new mean) instead of fetching them again -- one device-scope round trip per
+// task instead of two.  The tail stream's raw values wait in LDS (pass 1 writes them).
+template <int NS>
+__device__ __forceinline__ void nmc_hyper_once(const Dev& d, const double* src, int cb, int t,
+                                               double* lds, const nmc_lds_layout& L, int q) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int W = blockDim.x >> 6;
+  const int P = d.P, G = d.G, C = d.C, nl = d.nleaf, ncol = 8 + d.ntail;
+  const int per = 8 + (d.ntail ? 1 : 0);
+  const int c = nmc_lane_chain(d, cb, lane);
+  const int cc = c < C ? c : C - 1;
+  const int sbeg = q * nl * per, nst = (q + 1) * nl * per;
+  struct Strm {
+    int j, pl, m, m8;
+    const double* xp;
+  };
+  auto strm = [&](int s) {
+    Strm r;
+    r.j = s % per;
+    r.pl = s / per;
+    const int lf = r.pl % nl;
+    const int a = nl == 1 ? 0 : d.leaf[lf];
+    r.m = nl == 1 ? G : d.leaf[lf + 1] - a;
+    r.m8 = r.m >= 8 ? r.m - r.m % 8 : 0;
+    r.xp = src + ((size_t)q * G + a) * C + cc;
+    return r;
+  };
+  // one round: this wave's streams w, w + W, ..., w + (NS-1) W of [sbeg, nst)
+  static_assert(NS >= 1, "streams per wave");
+  double v[NS][16];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const int s = sbeg + w + k * W;
+    const Strm r = strm(s < nst ? s : sbeg);
+    const int cnt = s < nst && r.j < 8 ? r.m8 >> 3 : 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      v[k][u] = u < cnt ? nmc_ldv<NMC_SRC_SC1>(r.xp + (size_t)(r.j + 8 * u) * C) : 0.0;
+  }
+  auto pass = [&](bool sq) {
+    const double mu = sq ? lds[(L.hyp + NMC_HY_MU * P + q) * 64 + lane] : 0.0;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const int s = sbeg + w + k * W;
+      if (s >= nst) continue;
+      const Strm r = strm(s);
+      double* out = lds + (size_t)(L.hst + r.pl * ncol) * 64 + lane;
+      if (r.j < 8) {
+        const int cnt = r.m8 >> 3;
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          if (u < cnt) {
+            double x = v[k][u];
+            if (sq) {
+              x = x - mu;
+              x = x * x;
+            }
+            acc = u == 0 ? x : acc + x;
+          }
+        }
+        out[r.j * 64] = acc;
+      } else {   // the tail: raw values in pass 1, their squares about mu in pass 2
+        for (int u = r.m8; u < r.m; ++u) {
+          double x = sq ? out[(8 + u - r.m8) * 64] : nmc_ldv<NMC_SRC_SC1>(r.xp + (size_t)u * C);
+          if (sq) {
+            x = x - mu;
+            x = x * x;
+          }
+          out[(8 + u - r.m8) * 64] = x;
+        }
+      }
+    }
+  };
+  // (a wave holds NS streams: the whole parameter's streams in one round)
+  pass(false);
+  __syncthreads();
+  if (w == 0) {
+    const double tot = nmc_hyper_combine(d, lds, L, q, lane);
+    const double sdm = lds[(L.hyp + NMC_HY_SDM * P + q) * 64 + lane];
+    const double hz = lds[L.hv * 64 + (q * 64 + lane) * 2];
+    lds[(L.hyp + NMC_HY_MU * P + q) * 64 + lane] = tot / G + sdm * hz;   // mu ~ N(mean, s2/G)
+  }
+  __syncthreads();
+  pass(true);
+  __syncthreads();
+  if (w == 0) {
+    const bool own = nmc_lane_owns(d, c, lane);
+    const int row = nmc_record_row(d, t);
+    const double ss = nmc_hyper_combine(d, lds, L, q, lane);
+    const double hat = ss / (double)(G - 1);
+    const double scale = d.ha * hat;
+    const double hx = lds[L.hv * 64 + (q * 64 + lane) * 2 + 1];
+    // scipy invgamma.rvs: (1/gammainccinv(a, U)) * scale + loc; loc when scale == 0
+    const double s2n = scale == 0.0 ? 0.0 : (1.0 / hx) * scale;
+    const double sdn = sqrt(s2n);
+    const double lsd = log(sdn);
+    const double m = lds[(L.hyp + NMC_HY_MU * P + q) * 64 + lane];
+    lds[(L.hyp + NMC_HY_SD * P + q) * 64 + lane] = sdn;
+    lds[(L.hyp + NMC_HY_LSD * P + q) * 64 + lane] = lsd;
+    lds[(L.hyp + NMC_HY_S2 * P + q) * 64 + lane] = s2n;
+    lds[(L.hyp + NMC_HY_ISD * P + q) * 64 + lane] = 1.0 / sdn;
+    if (own) {
+      const size_t ho = nmc_hslot(d, t) + (size_t)q * C + c;
+      __hip_atomic_store(d.mu + ho, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.s2 + ho, s2n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.hsd + ho, sdn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.hlsd + ho, lsd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (row >= 0) {
+        double* out = d.samples + ((size_t)row * d.cols + (size_t)q * (G + 2)) * C + c;
+        out[0] = m;
+        out[C] = s2n;
+      }
+    }
+  }
+}
+
 // SYNC_OWN's Gibbs workgroup kb = (chain block, parameter q), four waves: every task (t, q)
 // of the launch in order, once its publication is complete -- HyperParameter.update
 // (:463-498) computed once per chain block, written through and counted ready (nmc_hrd)
 // for the likelihood workgroups' Gibbs waves.
-template <class Fam>
+// SEP: the Gibbs kernel of its own (nmc_k_sweep_gibbs, ~170 VGPRs free for the one-load
+// update); inside nmc_k_sweep the update streams its values twice (168-VGPR budget).
+template <class Fam, bool SEP>
 __device__ __forceinline__ void nmc_sweep_gibbs_wg(int kb, double* lds) {
   const nmc_sweep_args<Fam>* A = nmc_sweep_args_at<Fam>();
   const int lane = threadIdx.x & 63;
@@ -193,9 +316,21 @@ __device__ __forceinline__ void nmc_sweep_gibbs_wg(int kb, double* lds) {
     hy[(NMC_HY_LSD * P + q) * 64] = d.hlsd[ho];
     hy[(NMC_HY_S2 * P + q) * 64] = d.s2[ho];
   }
+#ifdef NMC_STAMPS   // chain block 0's Gibbs workgroups, iterations < 8 of the launch:
+                    // stamps[1024 + 4*4096 + ((t - i0) * 16 + 12 + q) * 4 + k]
+#define NMC_GSTAMP(k)                                                                        \
+  do {                                                                                       \
+    if (d.stamps && hcb == 0 && q < 4 && t - i0 < 8 && threadIdx.x == 0)                      \
+      d.stamps[1024 + 4 * 4096 + ((t - i0) * 16 + 12 + q) * 4 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define NMC_GSTAMP(k) do {} while (0)
+#endif
   for (int t = i0; t < i1; ++t) {
     A = nmc_sweep_args_at<Fam>();
+    NMC_GSTAMP(3);
     if (!nmc_wait_published(d, hcb, q, (unsigned)d.G * (unsigned)(t - i0 + 1), lds, H)) break;
+    NMC_GSTAMP(0);
     if (w == 0) {   // the task's variates and sqrt(s2 / G) of the previous update
       nmc_d2 hv;
       if (d.zin) {
@@ -214,14 +349,44 @@ __device__ __forceinline__ void nmc_sweep_gibbs_wg(int kb, double* lds) {
     __syncthreads();
     // HyperParameter.update (:463-498) for the chain block, written through to the global
     // slot of t (and the sample row); wave 0 stored it and counts it ready
-    nmc_hyper<NMC_SRC_SC1, 4, true>(d, (t & 1) ? d.vb1 : d.vb0, hcb, t, lds, H, true, q);
+#ifdef NMC_STAMPS   // the update's phases (entry 14 + q): pass 1, mean, pass 2
+    {
+      const double* src = (t & 1) ? d.vb1 : d.vb0;
+      auto gs2 = [&](int k) {
+        if (d.stamps && hcb == 0 && q < 2 && t - i0 < 8 && threadIdx.x == 0)
+          d.stamps[1024 + 4 * 4096 + ((t - i0) * 16 + 14 + q) * 4 + k] = __builtin_amdgcn_s_memtime();
+      };
+      nmc_hyper_streams<NMC_SRC_SC1, false, 4>(d, src, cc, lds, H, q);
+      __syncthreads();
+      gs2(0);
+      if (w == 0) {
+        const double tot = nmc_hyper_combine(d, lds, H, q, lane);
+        const double sdm = lds[(H.hyp + NMC_HY_SDM * P + q) * 64 + lane];
+        const double hz = lds[H.hv * 64 + (q * 64 + lane) * 2];
+        lds[(H.hyp + NMC_HY_MU * P + q) * 64 + lane] = tot / G + sdm * hz;
+      }
+      __syncthreads();
+      gs2(1);
+      nmc_hyper_streams<NMC_SRC_SC1, true, 4>(d, src, cc, lds, H, q);
+      __syncthreads();
+      gs2(2);
+      // (diagnostics only: the full update below runs on the same inputs)
+    }
+#endif
+    if (SEP && d.nleaf * (8 + (d.ntail ? 1 : 0)) <= W * 4)   // every stream in one round
+      nmc_hyper_once<4>(d, (t & 1) ? d.vb1 : d.vb0, hcb, t, lds, H, q);
+    else
+      nmc_hyper<NMC_SRC_SC1, 4, true>(d, (t & 1) ? d.vb1 : d.vb0, hcb, t, lds, H, true, q);
+    NMC_GSTAMP(1);
     if (w == 0) {
       nmc_drain_vm();
       if (lane == 0)
         __hip_atomic_fetch_add(nmc_hrd(d, hcb, q), 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     }
+    NMC_GSTAMP(2);
   }
+#undef NMC_GSTAMP
   nmc_drain_vm();
 #undef d
 }
@@ -234,7 +399,10 @@ template <class Fam>
 __global__ void __launch_bounds__(256) nmc_k_sweep_gibbs(nmc_sweep_args<Fam> a_arg) {
   (void)a_arg;
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  nmc_sweep_gibbs_wg<Fam>((int)blockIdx.x, lds);
+  // (its waves share a CU with two likelihood workgroups: issue ahead of their tile waves,
+  //  the update is on every step's critical path; NMC_NOPRIO bit 2 drops it)
+  if (!(a_arg.d.noprio & 2)) __builtin_amdgcn_s_setprio(3);
+  nmc_sweep_gibbs_wg<Fam, true>((int)blockIdx.x, lds);
 }
 
 template <class Fam, int MODE>
@@ -260,7 +428,7 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
   // ---- SYNC_OWN: the Gibbs workgroups (blocks RB * G .., unless Dev.gsep puts them in
   //      their own kernel, nmc_k_sweep_gibbs) ----
   if constexpr (OWN) if (!d.gsep && (int)blockIdx.x >= d.RB * d.G) {
-    nmc_sweep_gibbs_wg<Fam>((int)blockIdx.x - d.RB * d.G, lds);
+    nmc_sweep_gibbs_wg<Fam, false>((int)blockIdx.x - d.RB * d.G, lds);
     return;
   }
 

@@ -1,0 +1,8 @@
+#!/bin/bash
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 200 python tools/cfgbench.py cfg4 cfg4c64 > gpurun_out/u_cfg.jsonl 2> gpurun_out/u_cfg.err; echo "cfg rc=$?"
+NMC_NOPRIO=2 timeout -k 10 200 python tools/cfgbench.py cfg4 > gpurun_out/u_np.jsonl 2> gpurun_out/u_np.err; echo "np rc=$?"
+NMC_CTL_TILES=0 timeout -k 10 200 python tools/cfgbench.py cfg4 > gpurun_out/u_ct0.jsonl 2> gpurun_out/u_ct0.err; echo "ct0 rc=$?"

@@ -76,6 +76,21 @@ def main():
         rs = numpy.frombuffer(out, dtype=numpy.uint64)[17408:17920].reshape(8, 16, 4).astype(numpy.float64)
         tiles["restart%d" % si] = [[w] + [int(rs[si, w, k] - t0) for k in range(4)]
                                    for w in range(12) if rs[si, w, 0] > 0]
+    # the separate Gibbs kernel (chain block 0): per iteration it of the launch and q,
+    # [start of wait, published seen, update done, ready counted], absolute shader clocks
+    # rebased on the main kernel's step-0 origin of that iteration
+    gib = {}
+    for it in range(8):
+        for q in range(4):
+            row = rs[it, 12 + q]
+            if row[0] > 0 and "t0_%d" % (2 * it) in tiles:
+                base = tiles["t0_%d" % (2 * it)]
+                gib["it%d_q%d" % (it, q)] = [int(row[3] - base), int(row[0] - base),
+                                             int(row[1] - base), int(row[2] - base)]
+                if q < 2 and rs[it, 14 + q, 0] > 0:   # pass 1, mean, pass 2 (stamps build)
+                    gib["it%d_q%d_phases" % (it, q)] = [int(rs[it, 14 + q, k] - row[0])
+                                                        for k in range(3)]
+    tiles["gibbs"] = gib
     print(json.dumps(dict(pooling=pooling, N=N, config=eng.launch_config(), stamps=res,
                           tiles=tiles)))
     eng.close()
