@@ -101,6 +101,8 @@ struct Dev {
   int noprio;            // diagnostics: no issue priority for the latency-bound waves
   int sflags;            // nmc_k_step variants (bit-identical; NMC_STEP_FLAGS): 1 Gibbs payload
                          // via LDS-DMA, 2 next proposal formed before the barrier
+  int pubearly;          // nmc_k_sweep: the control counts the previous step's publication
+                         // before taking a tile (its store drained first), not after one
   int gsep;              // nmc_k_sweep SYNC_OWN: the Gibbs workgroups run as their own kernel
                          // (nmc_k_sweep_gibbs) on a second stream
   int ctiles;            // nmc_k_sweep, the control wave in the tile queue (NMC_CTL_TILES):

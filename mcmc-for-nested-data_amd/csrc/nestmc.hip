@@ -90,6 +90,7 @@ static void choose_geometry(nmc_ctx* x) {
   d.noprio = getenv("NMC_NOPRIO") ? atoi(getenv("NMC_NOPRIO")) : 0;   // diagnostics bits
   d.ctiles = getenv("NMC_CTL_TILES") ? atoi(getenv("NMC_CTL_TILES")) : 1;   // (Dev.ctiles)
   d.gtiles = getenv("NMC_GIBBS_TILES") ? atoi(getenv("NMC_GIBBS_TILES")) : 1;   // (Dev.gtiles)
+  d.pubearly = 0;   // (Dev.pubearly: set with the geometry, NMC_PUB_EARLY overrides)
   d.hlds = d.naux > 0 && d.G <= 128 && lds_bytes_for(x, 1, d.rows_lds) <= (size_t)160 * 1024 &&
            !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
   // G <= 64: the Gibbs wave fetches a task's values into registers (one sc1 round trip)
@@ -176,6 +177,11 @@ static void choose_geometry(nmc_ctx* x) {
       x->sweep = true;
       d.W = sw;
     }
+    // SYNC_OWN: the count of a publication is the start of the Gibbs workgroups' update,
+    // which every step two later waits for -- count it before the control's first tile
+    // (cfg-4 shard 30.8 vs 32.4 us/iter, profiles/r04u_ab.txt); elsewhere after it
+    d.pubearly = run_mode(x) == NMC_MODE_SYNC_OWN ? 1 : 0;
+    if (const char* e = getenv("NMC_PUB_EARLY")) d.pubearly = atoi(e) != 0;
     // (SYNC_OWN's Gibbs workgroups go into their own kernel, Dev.gsep, only when the one
     // grid cannot be resident: nmc_create; NMC_GSEP=1 forces it)
     if (x->sweep && x->pooling == NMC_POOL_PARTIAL && d.G > 128 &&

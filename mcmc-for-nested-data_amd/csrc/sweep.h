@@ -650,6 +650,10 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         // control's count of the previous step's published value waits for its store there,
         // off the step's critical path
         bool first = true;
+        if (d.pubearly) {   // (Dev.pubearly: before this wave's first entry)
+          after_first();
+          first = false;
+        }
         while (kq >= 0) {
           const unsigned kn = cpick ? 0u : issue();
           NMC_TILE_STAMP(kq, 0);
