@@ -103,6 +103,7 @@ struct Dev {
                          // via LDS-DMA, 2 next proposal formed before the barrier
   int pubearly;          // nmc_k_sweep: the control counts the previous step's publication
                          // before taking a tile (its store drained first), not after one
+  int gwaves;            // waves of nmc_k_sweep_gibbs (4)
   int gsep;              // nmc_k_sweep SYNC_OWN: the Gibbs workgroups run as their own kernel
                          // (nmc_k_sweep_gibbs) on a second stream
   int ctiles;            // nmc_k_sweep, the control wave in the tile queue (NMC_CTL_TILES):

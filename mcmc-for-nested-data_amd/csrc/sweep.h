@@ -293,9 +293,10 @@ __device__ __forceinline__ void nmc_hyper_once(const Dev& d, const double* src, 
 // of the launch in order, once its publication is complete -- HyperParameter.update
 // (:463-498) computed once per chain block, written through and counted ready (nmc_hrd)
 // for the likelihood workgroups' Gibbs waves.
-// SEP: the Gibbs kernel of its own (nmc_k_sweep_gibbs, ~170 VGPRs free for the one-load
-// update); inside nmc_k_sweep the update streams its values twice (168-VGPR budget).
-template <class Fam, bool SEP>
+// GW: the waves of the Gibbs kernel of its own (nmc_k_sweep_gibbs: the one-load update, four
+// streams per wave on 4 waves, two on 8); 0: inside nmc_k_sweep, where the update streams its
+// values twice (168-VGPR budget shared with the likelihood code).
+template <class Fam, int GW>
 __device__ __forceinline__ void nmc_sweep_gibbs_wg(int kb, double* lds) {
   const nmc_sweep_args<Fam>* A = nmc_sweep_args_at<Fam>();
   const int lane = threadIdx.x & 63;
@@ -373,10 +374,11 @@ __device__ __forceinline__ void nmc_sweep_gibbs_wg(int kb, double* lds) {
       // (diagnostics only: the full update below runs on the same inputs)
     }
 #endif
-    if (SEP && d.nleaf * (8 + (d.ntail ? 1 : 0)) <= W * 4)   // every stream in one round
-      nmc_hyper_once<4>(d, (t & 1) ? d.vb1 : d.vb0, hcb, t, lds, H, q);
+    if (GW > 0 && d.nleaf * (8 + (d.ntail ? 1 : 0)) <= 16)   // every stream in one round
+      nmc_hyper_once<GW == 8 ? 2 : 4>(d, (t & 1) ? d.vb1 : d.vb0, hcb, t, lds, H, q);
     else
-      nmc_hyper<NMC_SRC_SC1, 4, true>(d, (t & 1) ? d.vb1 : d.vb0, hcb, t, lds, H, true, q);
+      nmc_hyper<NMC_SRC_SC1, GW == 8 ? 1 : 4, true>(d, (t & 1) ? d.vb1 : d.vb0, hcb, t, lds, H,
+                                                    true, q);
     NMC_GSTAMP(1);
     if (w == 0) {
       nmc_drain_vm();
@@ -395,14 +397,15 @@ __device__ __forceinline__ void nmc_sweep_gibbs_wg(int kb, double* lds) {
 // of four waves, the small nmc_lds carve), launched on a second stream beside
 // nmc_k_sweep's RB * G likelihood workgroups: co-resident with two 61-KB likelihood
 // workgroups per CU where one kernel with a single LDS size would not be.
-template <class Fam>
-__global__ void __launch_bounds__(256) nmc_k_sweep_gibbs(nmc_sweep_args<Fam> a_arg) {
+// GW: its waves (4: four streams per wave, every stream of a 256-group update in one round)
+template <class Fam, int GW>
+__global__ void __launch_bounds__(64 * GW) nmc_k_sweep_gibbs(nmc_sweep_args<Fam> a_arg) {
   (void)a_arg;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   // (its waves share a CU with two likelihood workgroups: issue ahead of their tile waves,
   //  the update is on every step's critical path; NMC_NOPRIO bit 2 drops it)
   if (!(a_arg.d.noprio & 2)) __builtin_amdgcn_s_setprio(3);
-  nmc_sweep_gibbs_wg<Fam, true>((int)blockIdx.x, lds);
+  nmc_sweep_gibbs_wg<Fam, GW>((int)blockIdx.x, lds);
 }
 
 template <class Fam, int MODE>
@@ -428,7 +431,7 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
   // ---- SYNC_OWN: the Gibbs workgroups (blocks RB * G .., unless Dev.gsep puts them in
   //      their own kernel, nmc_k_sweep_gibbs) ----
   if constexpr (OWN) if (!d.gsep && (int)blockIdx.x >= d.RB * d.G) {
-    nmc_sweep_gibbs_wg<Fam, false>((int)blockIdx.x - d.RB * d.G, lds);
+    nmc_sweep_gibbs_wg<Fam, 0>((int)blockIdx.x - d.RB * d.G, lds);
     return;
   }
 

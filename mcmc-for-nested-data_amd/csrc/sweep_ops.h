@@ -23,6 +23,13 @@ static const void* nmc_sweep_kernel(int mode) {
   return nullptr;
 }
 
+// (four waves: an eight-wave form with two streams per wave needs <= 88 VGPRs to sit beside
+//  two likelihood workgroups and spilled at that budget)
+template <class Fam>
+static const void* nmc_sweep_gibbs_kernel(int) {
+  return (const void*)nmc_k_sweep_gibbs<Fam, 4>;
+}
+
 // NMC_OP_RUN / NMC_OP_CAN_PERSIST / NMC_OP_CAPACITY of a context whose loop runs nmc_k_sweep.
 template <class Fam>
 static int nmc_sweep_call_t(nmc_ctx* x, const Fam& fam, NmcCall& c) {
@@ -40,8 +47,8 @@ static int nmc_sweep_call_t(nmc_ctx* x, const Fam& fam, NmcCall& c) {
           hipEventRecord(x->gev[0], x->stream);
           hipStreamWaitEvent(x->gstream, x->gev[0], 0);
           const unsigned nb = grid.x / (unsigned)d.G;   // chain blocks of this launch
-          hipLaunchKernel((const void*)nmc_k_sweep_gibbs<Fam>, dim3(nb * d.P), dim3(256), args,
-                          sweep_gibbs_lds_bytes(x), x->gstream);
+          hipLaunchKernel(nmc_sweep_gibbs_kernel<Fam>(d.gwaves), dim3(nb * d.P),
+                          dim3(64 * d.gwaves), args, sweep_gibbs_lds_bytes(x), x->gstream);
           hipLaunchKernel(nmc_sweep_kernel<Fam>(mode), grid, block, args, lds, x->stream);
           hipEventRecord(x->gev[1], x->gstream);
           hipStreamWaitEvent(x->stream, x->gev[1], 0);
@@ -69,17 +76,24 @@ static int nmc_sweep_call_t(nmc_ctx* x, const Fam& fam, NmcCall& c) {
         // VGPRs: three waves per SIMD) for one four-wave Gibbs workgroup; the launches run
         // the chain blocks in such batches (nmc_run_launches)
         int ng = 0;
+        const void* gk = nmc_sweep_gibbs_kernel<Fam>(x->d.gwaves);
+        const int gw = x->d.gwaves;
+        hipFuncAttributes am{}, ag{};
         const bool gok = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                             &ng, (const void*)nmc_k_sweep_gibbs<Fam>, 256,
-                             sweep_gibbs_lds_bytes(x)) == hipSuccess && ng >= 1;
+                             &ng, gk, 64 * gw, sweep_gibbs_lds_bytes(x)) == hipSuccess &&
+                         ng >= 1 && hipFuncGetAttributes(&am, k) == hipSuccess &&
+                         hipFuncGetAttributes(&ag, gk) == hipSuccess;
+        // VGPRs per SIMD (512 per lane, allocated in 8s) and wave slots (8 per SIMD)
+        auto vg = [](int r) { return (r + 7) / 8 * 8; };
         const int64_t cap = (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
         int best = 0;
         for (int b = 1; gok && b <= x->d.RB; ++b) {
           const int64_t wg = (int64_t)b * x->d.G;
           const int64_t per = (wg + x->ncu - 1) / x->ncu;
+          const int64_t mw = (per * x->d.W + 3) / 4, gws = (gw + 3) / 4;   // waves per SIMD
           if (wg <= cap &&
               per * (int64_t)nmc_persist_lds(x) + sweep_gibbs_lds_bytes(x) <= (size_t)160 * 1024 &&
-              per * x->d.W + 4 <= 12)
+              mw * vg(am.numRegs) + gws * vg(ag.numRegs) <= 512 && mw + gws <= 8)
             best = b;
         }
         x->sweep_batch = best;
