@@ -104,6 +104,8 @@ struct Dev {
   int pubearly;          // nmc_k_sweep: the control counts the previous step's publication
                          // before taking a tile (its store drained first), not after one
   int gwaves;            // waves of nmc_k_sweep_gibbs (4)
+  int nstatic;           // nmc_k_run: waves 2.. start on static tile entries (W - 2; 0 off,
+                         // NMC_STATIC_TILES=0)
   int gsep;              // nmc_k_sweep SYNC_OWN: the Gibbs workgroups run as their own kernel
                          // (nmc_k_sweep_gibbs) on a second stream
   int ctiles;            // nmc_k_sweep, the control wave in the tile queue (NMC_CTL_TILES):
@@ -1722,7 +1724,10 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     for (int j = 0; j < Fam::NACC; ++j)   // x + (-0.0) == x: the fixed slot sum
       for (int k = nt; k < NMC_NSLOT; ++k) lds[(L.part + j * NMC_NSLOT + k) * 64 + lane] = -0.0;
     nmc_drain_vm();
-    lds[L.flag * 64 + lane] = 0.0;       // (also zeroes both tile counters)
+    lds[L.flag * 64 + lane] = 0.0;
+    // both tile counters start at the static entries: waves 2 .. W-1 begin on entries
+    // 0 .. W-3 by rank, without a take (every wave from 2 on runs lik_tiles in every mode)
+    if (lane < 2) tcnt[lane] = (unsigned)(d.nstatic && W > 2 ? W - 2 : 0);
   }
   __syncthreads();
   NMC_RUN_SL(1);
@@ -1798,7 +1803,9 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     // d.zin: queue entry 0 is the next step's variate job, entries 1.. the tiles
     const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
     const int zj = NMC_ZIN_BUILD && d.zin && tn < i1 ? 1 : 0;
-    int kq = (int)__builtin_amdgcn_readlane(grab(), 0);
+    // (waves 2.. start on their static entry: one LDS round trip off the step's restart)
+    int kq = d.nstatic && w >= 2 ? (w - 2 < nt + zj ? w - 2 : nt + zj)
+                                 : (int)__builtin_amdgcn_readlane(grab(), 0);
     while (kq < nt + zj) {
       const unsigned kn = grab();
       if (kq < zj) {   // the variate job: {z, log u} of the next step -> the other slot
@@ -2185,7 +2192,8 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       // ---- control wave: group log-likelihood of the proposal (tiles in order) and
       //      the Metropolis decision, one chain per lane (:334-383) ----
       if (ctl) {
-        if (lane == 0) tcnt[sp] = 0u;   // this step's tiles are all taken; reused at step +2
+        // this step's tiles are all taken; reused at step +2 (from the static entries on)
+        if (lane == 0) tcnt[sp] = (unsigned)(d.nstatic && W > 2 ? W - 2 : 0);
         double acc[Fam::NACC];
 #pragma unroll
         for (int j = 0; j < Fam::NACC; ++j) {

@@ -92,6 +92,7 @@ static void choose_geometry(nmc_ctx* x) {
   d.gtiles = getenv("NMC_GIBBS_TILES") ? atoi(getenv("NMC_GIBBS_TILES")) : 1;   // (Dev.gtiles)
   d.pubearly = 0;   // (Dev.pubearly: set with the geometry, NMC_PUB_EARLY overrides)
   d.gwaves = 4;   // (waves of nmc_k_sweep_gibbs)
+  d.nstatic = getenv("NMC_STATIC_TILES") ? atoi(getenv("NMC_STATIC_TILES")) != 0 : 1;
   d.hlds = d.naux > 0 && d.G <= 128 && lds_bytes_for(x, 1, d.rows_lds) <= (size_t)160 * 1024 &&
            !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
   // G <= 64: the Gibbs wave fetches a task's values into registers (one sc1 round trip)
