@@ -16,7 +16,9 @@ FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fP
 
 
 def usage(tu):
-    extra = ["-mllvm", "-disable-machine-licm"] if tu.startswith("sweep_") else []
+    # (as the Makefile: the sweep TUs and fam_linreg / fam_gauss_mean without machine LICM)
+    extra = (["-mllvm", "-disable-machine-licm"]
+             if tu.startswith("sweep_") or tu in ("fam_linreg", "fam_gauss_mean") else [])
     r = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *extra, "-c", tu + ".hip", "-o",
                         "/tmp/_regusage.o"], cwd=CSRC, capture_output=True, text=True)
     rows, cur = [], None
