@@ -38,6 +38,28 @@ def _check_vs_oracle(dev, nested, st, sel, chain_ids, n_iter, seed, **kw):
     assert _close(rows[sel], orows)
 
 
+def test_cfg4_sweep_resident_batches_of_chain_blocks(gpu_lib):
+    """Three chain blocks of the cfg-4 geometry (192 chains x 256 groups x 2000 rows): the
+    sweep with its Gibbs kernel fits two chain blocks at a time, so each launch runs the
+    chain blocks in resident batches (2 + 1) -- bit for bit nmc_k_run's single grid,
+    across three launches (counters carried over)."""
+    G, N, n_iter, seed, C = 256, 2000, 6, 41, 192
+    x, y, _, _ = data.linreg(G, N, seed=7)
+    fam = LinearRegression.simple(x, y, sigma=1.0)
+    sizes = [N] * G
+    st, _ = partial_state(fam, sizes, C, 2)
+    sel = numpy.arange(C)
+    bat = run_engine(fam, sizes, st, sel, 0, n_iter, seed, launch_iters=2)
+    cfg = bat[3]
+    assert cfg["kernel"].startswith("nmc_k_sweep<") and cfg["mode"] == "NMC_MODE_SYNC_OWN", cfg
+    assert cfg["chain_blocks"] == 3 and cfg["chain_blocks_per_launch"] < 3, cfg
+    ref = run_engine(fam, sizes, st, sel, 0, n_iter, seed, launch_iters=2,
+                     env={"NMC_SWEEP": "0"})
+    assert ref[3]["kernel"].startswith("nmc_k_run<"), ref[3]
+    for k in range(3):
+        assert numpy.array_equal(bat[k], ref[k], equal_nan=True), k
+
+
 @pytest.mark.parametrize("G", [129, 256])
 def test_cfg4_geometry_multileaf_gibbs(gpu_lib, G):
     N, n_iter, seed = 2000, 8, 31
