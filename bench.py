@@ -100,6 +100,9 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the two rocprofv3 PMC passes that measure HBM traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--spawn-dry-run", action="store_true",
+                    help="(tests) every spawned rank prints its shard and exits before any "
+                         "HIP call")
     a = ap.parse_args()
     wl = dict(WORKLOADS[a.workload])
     if a.chains:
@@ -224,14 +227,36 @@ def _cpu_worker(args):
     return _cpu_loop((wl, chain, iters, barrier))
 
 
+def cgroup_cpu_quota():
+    """CPUs the cgroup's CFS quota grants this process (cgroup v2 cpu.max, or v1
+    cpu.cfs_quota_us / cpu.cfs_period_us), or None when unlimited / unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                return float(q) / float(per)
+            return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read().strip())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read().strip())
+        return q / per if q > 0 and per > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_cores():
-    """Cores this process may run on (the affinity mask), capped by OMP_NUM_THREADS when the
-    host sets it (the GPU box gives each GPU a 16-core share and says so there)."""
-    n = len(os.sched_getaffinity(0))
-    omp = os.environ.get("OMP_NUM_THREADS")
-    if omp and omp.isdigit() and int(omp) > 0:
-        n = min(n, int(omp))
-    return max(1, n), len(os.sched_getaffinity(0))
+    """The host cores this process may really use: the affinity mask, bounded by the cgroup's
+    CPU quota when one is set (a quota of 16 CPUs runs 16 cores' worth of work however many
+    processes share it).  OMP_NUM_THREADS is a BLAS-thread knob, not a core budget, and is
+    ignored.  Returns (cores, affinity mask size, quota or None)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    n = aff if quota is None else min(aff, max(1, int(math.floor(quota + 1e-9))))
+    return max(1, n), aff, quota
 
 
 def cpu_baseline(wl, window_s):
@@ -240,7 +265,7 @@ def cpu_baseline(wl, window_s):
     lasts ``window_s``; chain init is outside the timed window."""
     import multiprocessing as mp
     from oracle import restatement as rs
-    cores, affinity = cpu_cores()
+    cores, affinity, quota = cpu_cores()
     # warm the imports and size the sample: init one chain, one untimed iteration, then
     # time two
     nested, names, priors, ranges = _oracle_problem(wl)
@@ -265,11 +290,14 @@ def cpu_baseline(wl, window_s):
     rate = sum(per)
     out = {"value": rate, "unit": "chain*group*iter/s", "cores": cores, "kind": "port",
            "sample": "%d chains x %d iterations of the %s workload (%d groups x %d obs, %s "
-                     "pooling) in the numpy oracle, one process per chain on %d cores (affinity "
-                     "mask %d); timed loop only (init excluded), each process's loop rate "
-                     "summed; %.1f s from the first start to the last end"
+                     "pooling) in the numpy oracle, one process per chain on %d cores (the "
+                     "process's affinity mask holds %d cores; cgroup CPU quota %s); timed loop "
+                     "only (init excluded), each process's loop rate summed; %.1f s from the "
+                     "first start to the last end"
                      % (cores, iters, wl.get("name", "?"), wl["groups"], wl["obs"],
-                        wl["pooling"], cores, affinity, wall),
+                        wl["pooling"], cores, affinity,
+                        "none" if quota is None else "%.1f CPUs" % quota, wall),
+           "affinity_cores": affinity, "cgroup_quota_cpus": quota,
            "timed_seconds": wall, "iterations": iters,
            "value_wall": cores * wl["groups"] * iters / wall,
            "per_process_min_max": [per[0], per[-1]]}
@@ -378,6 +406,57 @@ def fam_instance(kernel):
     return kernel[i + 1:].strip()
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args):
+    """``--gpus N`` (N > 1) without a launcher: this process starts N ranks itself, one per
+    GPU, as child processes with the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT) -- before it makes any HIP call -- and relays rank 0's JSON
+    line; any failed rank fails the run.  The CPU-baseline leg runs here, before the
+    spawn, and is attached to the line (the ranks skip it and the PMC passes).  Replaces the
+    reference's process fan-out (posteriorSampling.py:182-201) at the GPU level."""
+    import subprocess
+    cpu = None
+    if args.cpu_seconds > 0 and not args.spawn_dry_run:
+        try:
+            cpu = cpu_baseline(args.wl, args.cpu_seconds)
+        except Exception as e:
+            cpu = {"value": None, "error": repr(e)}
+    n = args.gpus
+    port, bport = _free_port(), _free_port()
+    argv = [sys.executable, os.path.abspath(__file__)] + [
+        a for a in sys.argv[1:] if a not in ("--no-pmc",)] + ["--no-pmc", "--cpu-seconds", "0"]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   NMC_BOOTSTRAP_PORT=str(bport))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen(argv, env=env, stdout=subprocess.PIPE, text=True))
+    outs = [p.communicate()[0] for p in procs]
+    bad = [(r, p.returncode) for r, p in enumerate(procs) if p.returncode != 0]
+    if bad:
+        print("bench.py: rank(s) failed: %s" % bad, file=sys.stderr)
+        return 1
+    lines = [[ln for ln in o.splitlines() if ln.startswith("{")] for o in outs]
+    if not lines[0]:
+        print("bench.py: rank 0 printed no JSON line", file=sys.stderr)
+        return 1
+    out = json.loads(lines[0][-1])
+    if args.spawn_dry_run:
+        out["ranks"] = [json.loads(ls[-1]) for ls in lines]
+    else:
+        out["cpu_baseline"] = cpu
+        out["launcher"] = "bench.py --gpus %d: %d child ranks" % (n, n)
+    print(json.dumps(out))
+    return 0
+
+
 def main():
     args = parse()
     wl = args.wl
@@ -385,8 +464,18 @@ def main():
     world, rank, local = dist_env()
     if args.pmc_child:
         return pmc_child(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args)
     if args.gpus != world and world > 1:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    if args.spawn_dry_run:
+        # (tests) the rank's view of the job, before any HIP call
+        c0, C = rank_chains(wl, world, rank)
+        print(json.dumps({"dry_run": True, "rank": rank, "local_rank": local, "n_gpus": world,
+                          "workload": args.workload, "chain_base": c0, "chains": C,
+                          "chains_total": job_chains(wl, world), "scaling": wl["scaling"],
+                          "libnestmc_mapped": "libnestmc" in open("/proc/self/maps").read()}))
+        return 0
     # host-side legs first, before this process initialises the GPU: the PMC passes
     # run this script as rocprofv3 children, the CPU baseline forks a process pool
     pmc, cpu = None, None
@@ -568,4 +657,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -47,7 +47,8 @@ NMC_HD double nmc_exp_neg(double x) {   // exp(x) for x <= 0 (NaN propagates)
   p = fma(p, r, 0.5);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
-  return ldexp(p, (int)kd);
+  // (a NaN x leaves kd NaN: it is never converted to int -- p is NaN, and so is the result)
+  return ldexp(p, kd == kd ? (int)kd : 0);
 }
 
 NMC_HD double nmc_log1p_unit(double e) {   // log1p(e) for e in [0, 1] (NaN propagates)

@@ -33,10 +33,15 @@ class HostGroup:
     ``broadcast(data, src=0)``, ``gather(data)`` (root 0), ``all_gather(data)``,
     ``barrier()`` and ``max_float(v)`` move ``bytes`` between the ranks; every rank must
     call the same sequence.  Rank 0 listens on ``addr:port``; the others connect (retrying
-    until ``timeout`` seconds) and announce their rank.
+    until ``connect_timeout`` seconds) and announce their rank.  Every collective then waits
+    up to ``timeout`` seconds for its peers (default 1800 s, gloo's default, or
+    NMC_HOSTGROUP_TIMEOUT): a rank may reach a barrier minutes after the others (chain
+    init, hiprtc compilation of a user family).
     """
 
-    def __init__(self, world, rank, addr=None, port=None, timeout=120.0):
+    def __init__(self, world, rank, addr=None, port=None, timeout=None, connect_timeout=120.0):
+        if timeout is None:
+            timeout = float(os.environ.get("NMC_HOSTGROUP_TIMEOUT", "1800"))
         self.world, self.rank = int(world), int(rank)
         addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
         if port is None:
@@ -48,7 +53,7 @@ class HostGroup:
         self.sock = None         # other ranks: the connection to rank 0
         if self.world == 1:
             return
-        deadline = time.time() + timeout
+        deadline = time.time() + connect_timeout
         if self.rank == 0:
             srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)

@@ -74,3 +74,37 @@ def test_max_over_ranks_two_processes():
 def test_family_instance_of_kernel_name(kernel, inst):
     """The roofline's per-row instruction count is keyed by the step kernel's family."""
     assert bench.fam_instance(kernel) == inst
+
+
+@pytest.mark.parametrize("name", sorted(bench.WORKLOADS))
+@pytest.mark.parametrize("n", [2, 4])
+def test_gpus_flag_spawns_ranks(name, n):
+    """``bench.py --gpus N`` without a launcher starts N ranks itself (torchrun's env, one
+    per GPU) before any HIP call, and relays rank 0's line with n_gpus == N; every rank
+    holds its own shard of the job (dry run: the ranks stop before GPU init)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n),
+                        "--workload", name, "--spawn-dry-run"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    import json
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == n and line["rank"] == 0
+    ranks = line["ranks"]
+    assert [r["rank"] for r in ranks] == list(range(n))
+    assert [r["local_rank"] for r in ranks] == list(range(n))
+    assert all(r["n_gpus"] == n and not r["libnestmc_mapped"] for r in ranks)
+    wl = dict(bench.WORKLOADS[name])
+    for r in ranks:
+        assert (r["chain_base"], r["chains"]) == bench.rank_chains(wl, n, r["rank"])
+    covered = sorted(c for r in ranks for c in range(r["chain_base"], r["chain_base"] + r["chains"]))
+    assert covered == list(range(bench.job_chains(wl, n)))
+
+
+def test_cpu_cores_is_the_real_budget():
+    """cpu_baseline's core count is the affinity mask bounded by the cgroup CPU quota, not
+    OMP_NUM_THREADS."""
+    cores, aff, quota = bench.cpu_cores()
+    assert aff == len(os.sched_getaffinity(0))
+    assert cores == (aff if quota is None else min(aff, max(1, int(quota))))
