@@ -15,6 +15,7 @@
 
 #include "../../include/nestmc.h"
 #include "kernels.h"
+#include "duo.h"
 #include "step.h"
 #include "sweep.h"
 
@@ -66,6 +67,8 @@ struct nmc_ctx {
   bool step_ok = false;                   // nmc_k_step where it applies (NMC_STEP=1)
   bool sweep = false;                     // nmc_k_sweep runs the loop (choose_geometry)
   bool no_sweep = false;                  // (its grid could not be resident: nmc_k_run)
+  bool duo = false;                       // nmc_k_duo runs the loop (choose_geometry)
+  bool no_duo = false;                    // (its grid could not be resident: nmc_k_run)
 };
 
 static inline double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->d.vb0; }
@@ -80,6 +83,7 @@ static inline size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
              .total * 512;
 }
 static inline int run_mode(const nmc_ctx* x) {
+  if (x->duo) return NMC_MODE_DUO;
   if (x->pooling != NMC_POOL_PARTIAL) return x->d.CL == 32 ? NMC_MODE_HALF : NMC_MODE_NOPOOL;
   if (x->sweep)
     return x->d.G <= 64 ? NMC_MODE_SYNC_REG : x->d.G <= 128 ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC_OWN;
@@ -124,7 +128,13 @@ static inline int64_t sweep_grid(const nmc_ctx* x) {
          (x->pooling == NMC_POOL_PARTIAL && d.G > 128 && !d.gsep ? (int64_t)d.RB * d.P : 0);
 }
 
+// LDS of nmc_k_duo (duo.h): both half blocks' state, the control words and the group's rows
+static inline size_t duo_lds_bytes(const nmc_ctx* x) {
+  return (size_t)nmc_duo_lds(x->d.P, (int)(x->d.nmax * x->nf)).total * 8;
+}
+
 static inline size_t run_lds_bytes(const nmc_ctx* x) {
+  if (x->duo) return duo_lds_bytes(x);
   if (x->sweep) return sweep_lds_bytes(x);
   if (uses_step(x, run_mode(x))) return step_lds_bytes(x);
   return lds_bytes_for(x, x->persistent && x->d.hlds ? 1 : 0, x->d.rows_lds);
@@ -141,12 +151,13 @@ static inline int nmc_safe_blocks(const nmc_ctx* x, int nb) {
 }
 // mode of the persistent partial-pooling kernel (its occupancy query)
 static inline int nmc_persist_mode(const nmc_ctx* x) {
-  if (x->sweep) return run_mode(x);
+  if (x->sweep || x->duo) return run_mode(x);
   return x->d.hreg ? (x->d.hown ? NMC_MODE_SYNC_OWN : NMC_MODE_SYNC_REG)
                    : x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
 }
 // LDS of the persistent partial-pooling kernel (its occupancy query)
 static inline size_t nmc_persist_lds(const nmc_ctx* x) {
+  if (x->duo) return duo_lds_bytes(x);
   if (x->sweep) return sweep_lds_bytes(x);
   if (uses_step(x, nmc_persist_mode(x))) return step_lds_bytes(x);
   return lds_bytes_for(x, x->d.hlds && !x->d.hreg, x->d.rows_lds);

@@ -23,6 +23,10 @@ static const void* nmc_run_kernel_rl(int mode) {
 }
 template <class Fam>
 static const void* nmc_run_kernel(const nmc_ctx* x, int mode) {
+  if (mode == NMC_MODE_DUO) {   // (the {x, y} regression rows only: the host's condition)
+    if constexpr (Fam::ASM_ROWS) return (const void*)nmc_k_duo<Fam>;
+    return nullptr;
+  }
   if (uses_step(x, mode))
     return mode == NMC_MODE_NOPOOL ? (const void*)nmc_k_step<Fam, NMC_MODE_NOPOOL>
                                    : (const void*)nmc_k_step<Fam, NMC_MODE_SYNC_REG>;
@@ -47,8 +51,8 @@ static bool nmc_can_persist(nmc_ctx* x) {
   if (const char* e = getenv("NMC_PERSIST")) return atoi(e) != 0;
   int nb = 0;
   const void* k = nmc_run_kernel<Fam>(x, nmc_persist_mode(x));
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W, nmc_persist_lds(x)) !=
-      hipSuccess)
+  if (!k || hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W,
+                                                         nmc_persist_lds(x)) != hipSuccess)
     return false;
   return (int64_t)x->d.RB * x->d.G * x->d.S <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
 }

@@ -113,6 +113,7 @@ struct Dev {
                          // entries left (default), 2 like every other wave
   int gtiles;            // nmc_k_sweep, the Gibbs wave after its task (NMC_GIBBS_TILES): 0 no
                          // tiles, 1 as ctiles 1 (default)
+  int dkt;               // nmc_k_duo: likelihood tiles per ticket (NMC_DUO_KT)
   int rows_lds;          // 1: each workgroup stages its group's rows in LDS once per launch
   int tile;              // target rows per likelihood tile (nmc_tiles)
   unsigned* cnt;         // [CB][P][32] publish counters (persistent partial): zeroed at create,
@@ -1585,7 +1586,7 @@ enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
 typedef __attribute__((address_space(4))) const Dev* nmc_kdev_ptr;
 __device__ __forceinline__ const Dev* nmc_kdev() {
   nmc_kdev_ptr p = (nmc_kdev_ptr)__builtin_amdgcn_kernarg_segment_ptr();
-#if !defined(NMC_STAMPS) && !defined(NMC_NO_LAUNDER)
+#if !defined(NMC_STAMPS) && !defined(NMC_NO_LAUNDER) && !defined(NMC_DUO_STAMPS)
   // (the stamps build's divergent stamp stores make the backend move the laundered pointer
   //  to VGPRs, an illegal copy: diagnostics keep it plain; NMC_NO_LAUNDER: the A/B build)
   asm volatile("" : "+s"(p));

@@ -190,6 +190,32 @@ static void choose_geometry(nmc_ctx* x) {
         x->family < NMC_LL_USER_BASE && getenv("NMC_GSEP"))
       d.gsep = atoi(getenv("NMC_GSEP")) != 0;
   }
+
+  // nmc_k_duo (duo.h), opt-in NMC_DUO=1: partial pooling over G <= 64 groups with the {x, y}
+  // regression rows in LDS and no row split -- two half blocks of 32 chains per workgroup
+  // stepping on their own, no step barriers.  Bit-identical to nmc_k_run (the tests compare
+  // them) but measured slower at cfg 3: 8.2-8.9 against 7.6-7.7 us/iter
+  // (profiles/r05_duo/README.md).  NMC_DUO_WAVES sets the waves (4 role waves + likelihood).
+  x->duo = false;
+  const char* duo_env = getenv("NMC_DUO");
+  if (!x->no_duo && !x->sweep && !x->step_ok && duo_env && atoi(duo_env) != 0 &&
+      x->pooling == NMC_POOL_PARTIAL && x->family == NMC_LL_LINREG && x->nf == 2 &&
+      d.G >= 2 && d.G <= 64 && d.rows_lds && d.S == 1) {
+    x->duo = true;
+    d.W = NMC_DUO_THREADS / 64;
+    if (const char* e = getenv("NMC_DUO_WAVES")) {
+      const int v = atoi(e);
+      if (v >= 3 && v <= NMC_DUO_THREADS / 64) d.W = v;
+    }
+    d.CL = 64;
+    d.RB = (d.C + 63) / 64;
+    d.paired = 0;
+    d.dkt = 2;   // likelihood tiles per ticket
+    if (const char* e = getenv("NMC_DUO_KT")) {
+      const int v = atoi(e);
+      if (v >= 1 && v <= NMC_NSLOT) d.dkt = v;
+    }
+  }
 }
 
 // numpy's pairwise-sum recursion over G groups (numpy/_core/src/umath/loops_utils.h):
@@ -442,6 +468,11 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     }
     if (x->sweep && c.result != 1) {   // the sweep grid cannot be resident: nmc_k_run
       x->no_sweep = true;
+      choose_geometry(x);
+      if (int rc2 = nmc_call_family(x, c)) { nmc_destroy(x); return rc2; }
+    }
+    if (x->duo && c.result != 1) {     // the duo grid cannot be resident: nmc_k_run
+      x->no_duo = true;
       choose_geometry(x);
       if (int rc2 = nmc_call_family(x, c)) { nmc_destroy(x); return rc2; }
     }
@@ -891,7 +922,7 @@ int nmc_split_config(nmc_ctx* x, int* members, int* chain_blocks_per_launch) {
 int nmc_kernel_name(nmc_ctx* x, char* out, int cap) {
   static const char* const modes[] = {"NMC_MODE_NOPOOL", "NMC_MODE_LAUNCH", "NMC_MODE_SYNC",
                                       "NMC_MODE_SYNC_LDS", "NMC_MODE_SYNC_REG", "NMC_MODE_SYNC_OWN",
-                                      "NMC_MODE_HALF"};
+                                      "NMC_MODE_HALF", "NMC_MODE_DUO"};
   const int mode = run_mode(x);
   std::string fam;
   switch (x->family) {
@@ -899,6 +930,10 @@ int nmc_kernel_name(nmc_ctx* x, char* out, int cap) {
     case NMC_LL_GAUSS_MEAN: fam = "FamGaussMean<" + std::to_string(x->nf) + ">"; break;
     case NMC_LL_LOGISTIC: fam = "FamLogistic<" + std::to_string(x->nf) + ">"; break;
     default: fam = "FamUser"; break;
+  }
+  if (x->duo) {
+    snprintf(out, (size_t)(cap > 0 ? cap : 1), "%s", ("nmc_k_duo<" + fam + ">").c_str());
+    return cap < 1 ? fail(-1, "kernel name: cap < 1") : 0;
   }
   if (x->sweep) {
     snprintf(out, (size_t)(cap > 0 ? cap : 1), "%s",
