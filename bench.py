@@ -326,6 +326,11 @@ def pmc_child(args):
     eng.run(0, W)
     eng.run(W, W + K)
     eng.synchronize()
+    info = os.environ.get("NMC_PMC_INFO")
+    if info:   # what the counted launches ran (the parent reports it beside the bytes)
+        with open(info, "w") as f:
+            json.dump({"kernel": eng.launch_config()["kernel"],
+                       "gibbs_fallbacks": eng.gibbs_fallbacks()}, f)
     eng.close()
     assert _lib.device_count() >= 1
 
@@ -341,9 +346,9 @@ def measure_traffic(args):
     import shutil
     import subprocess
     import tempfile
-    out = {}
+    out, info = {}, {}
     base = tempfile.mkdtemp(prefix="nmc_pmc_", dir="/tmp")
-    env = dict(os.environ, TMPDIR="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp", NMC_PMC_INFO=os.path.join(base, "info.json"))
     try:
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(base, counter)
@@ -375,15 +380,29 @@ def measure_traffic(args):
             if len(rows) < 2:
                 return {"error": "no %s rows for the step kernel" % counter}
             out[counter] = sorted(rows)[-1][1]       # the K-iteration launch (the last)
+            try:
+                info = json.load(open(env["NMC_PMC_INFO"]))
+            except (OSError, ValueError):
+                pass
     finally:
         shutil.rmtree(base, ignore_errors=True)
     read_b = 2.0 * out["FETCH_SIZE"] * 1024.0
     write_b = out["WRITE_SIZE"] * 1024.0
-    return {"bytes_per_launch": read_b + write_b, "read_bytes": read_b, "write_bytes": write_b,
+    res = {}
+    if info.get("gibbs_fallbacks"):
+        # counter collection serializes dispatches: the Gibbs kernel of the G > 128 path did
+        # not run beside the step kernel, so the step kernel updated its Gibbs tasks itself
+        # (the same results) -- these bytes are that serialized form's
+        res["gibbs_fallbacks"] = info["gibbs_fallbacks"]
+        res["note"] = ("rocprofv3 --pmc serializes kernels: the counted launches ran the "
+                       "step kernel updating its own Gibbs tasks (nmc_gibbs_fallbacks = %d), "
+                       "not beside its Gibbs kernel" % info["gibbs_fallbacks"])
+    return dict(res, **{"bytes_per_launch": read_b + write_b, "read_bytes": read_b,
+                        "write_bytes": write_b,
             "fetch_size_kib_raw": out["FETCH_SIZE"], "write_size_kib_raw": out["WRITE_SIZE"],
             "iterations_per_launch": args.steps,
             "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) of this "
-                      "script's K-iteration launch; FETCH_SIZE x2 (gfx950), KiB -> bytes"}
+                      "script's K-iteration launch; FETCH_SIZE x2 (gfx950), KiB -> bytes"})
 
 
 def fam_instance(kernel):
@@ -585,13 +604,6 @@ def main():
         traffic = pmc["bytes_per_launch"] * iters_per_launch / pmc["iterations_per_launch"]
         hbm_meas = traffic / (avg_step_ms * 1e-3) / 1e9
 
-    if pmc and "error" in pmc and lc["mode"] == "NMC_MODE_SYNC_OWN" and kname.startswith("nmc_k_sweep"):
-        # rocprofv3 --pmc serializes dispatches; this path runs two kernels that wait on each
-        # other (nmc_k_sweep + nmc_k_sweep_gibbs on a second stream), so its counter passes
-        # time out by design: measure the counters on one chain block (one kernel) instead
-        pmc["note"] = ("counter collection serializes kernels; the two concurrent kernels of "
-                       "this path time out under it (tools/pmc_pass.sh on 64 chains measures "
-                       "the one-kernel form)")
     if rank == 0:
         desc = wl["desc"] % (wl["chains"], G, N, P)
         out = {

@@ -142,7 +142,8 @@ int nmc_obs_ll_rows(nmc_ctx* ctx, int row_begin, int n_rows, double* out);
 /* saveLogLikelihood=True (:890-891, :907-909): logLikelihood.<chain_ids[c]>.csv in dir
  * (a path prefix ending in '/') for every local chain and recorded row, "%f" joined by
  * ",".  Batches of rows are evaluated on the device and copied to pinned memory while
- * the host formats the previous batch with `threads` threads.                  */
+ * the host formats the previous batch with `threads` threads; a chain whose id is
+ * negative gets no file (a rank's padding chains).                             */
 int nmc_write_ll_csvs(nmc_ctx* ctx, const char* dir, const int32_t* chain_ids, int threads);
 
 /* Timing on the context's stream (hipEvents). */
@@ -174,6 +175,12 @@ int nmc_kernel_name(nmc_ctx* ctx, char* out, int cap);
  * them itself (no nmc_k_fill launch for them), 0 when nmc_k_fill writes them to a ring in
  * HBM first.  Both give the same bits (Parameter.propose :304-306, the accept draw :362). */
 int nmc_variate_source(nmc_ctx* ctx, int* in_kernel);
+/* Partial pooling over G > 128 groups runs the Gibbs update (HyperParameter.update
+ * :463-498, once per chain block) as a kernel of its own beside the step kernel; when the
+ * two did not run at the same time (a profiler or AMD_SERIALIZE_KERNEL serializes kernels)
+ * the step kernel updated that launch's tasks itself, with the same results.  *out = the
+ * (launch, chain block) pairs that did so since nmc_create (diagnostics and tests).     */
+int nmc_gibbs_fallbacks(nmc_ctx* ctx, int64_t* out);
 
 /* Sampler._printSample (:902-905) + _print (:933-936): append rows of local
  * chain c to a CSV file with the reference's "%i,%i,%f,..." formatting (and the

@@ -61,6 +61,9 @@ struct nmc_ctx {
   int64_t nmax_group = 0;                 // rows of the largest group
   int split_batch = 0;                    // row split: chain blocks per (resident) launch
   int sweep_batch = 0;                    // nmc_k_sweep with Dev.gsep: chain blocks per launch
+  unsigned gepoch = 0;                    // Dev.gsep launches so far (Dev.gep)
+  int gserial = 0;                        // tests (NMC_GSEP_SERIAL): the gsep kernels serialized
+                                          // on one stream, 1 Gibbs kernel first, 2 second
   volatile unsigned* tmo_host = nullptr;  // host view of d.tmo (coherent pinned memory)
   void* user = nullptr;                   // user family: its per-device kernel table (user.hip)
   double* user_k = nullptr;               // user family: device copy of the model constants

@@ -108,6 +108,13 @@ struct Dev {
                          // NMC_STATIC_TILES=0)
   int gsep;              // nmc_k_sweep SYNC_OWN: the Gibbs workgroups run as their own kernel
                          // (nmc_k_sweep_gibbs) on a second stream
+  // gsep progress without co-scheduling (sweep.h nmc_grole_*): per chain block a role word
+  // [63:32] launch epoch, [31:1] Gibbs workgroups started, [0] fallback -- if the Gibbs
+  // kernel has not started within gpat ticks (s_memrealtime, 100 MHz), the likelihood
+  // workgroups update every task themselves (bit-identical) and the Gibbs kernel leaves
+  unsigned long long* grole;   // [RB][16] (one 128-B line per chain block)
+  unsigned* gfb;         // chain-block launches that fell back, since create
+  unsigned gep, gpat;    // this launch's epoch (the host counts gsep launches), patience
   int ctiles;            // nmc_k_sweep, the control wave in the tile queue (NMC_CTL_TILES):
                          // 0 never, 1 only while the other waves have more than a round of
                          // entries left (default), 2 like every other wave
@@ -1456,8 +1463,11 @@ __device__ __forceinline__ void nmc_split_exchange(const Dev& d, int cb, int g, 
 // host plan d.leaf) as 8 interleaved streams carried across chunks plus its tail in
 // order, the leaves merged in numpy's recursion order (d.merge) -- the order of
 // nmc_hyper_compute and the oracle.  src: the parameter's [G][C] values + this chain.
+// CH: values per chunk (loads in flight together, 2 * CH VGPRs).
+template <int CH = 64>
 __device__ __forceinline__ double nmc_pairwise_stream(const Dev& d, const double* src, bool sq,
                                                       double mu) {
+  static_assert(CH % 8 == 0 && CH <= 64, "chunks of whole 8-value blocks");
   const int C = d.C, G = d.G, nl = d.nleaf;
   auto tr = [&](double v) {
     if (sq) {
@@ -1472,13 +1482,13 @@ __device__ __forceinline__ double nmc_pairwise_stream(const Dev& d, const double
     const int m = nl == 1 ? G : d.leaf[lf + 1] - a;
     const int m8 = m >= 8 ? m - m % 8 : 0;
     double r[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int e0 = 0; e0 < m8; e0 += 64) {
-      double x[64];
+    for (int e0 = 0; e0 < m8; e0 += CH) {
+      double x[CH];
 #pragma unroll
-      for (int k = 0; k < 64; ++k)
+      for (int k = 0; k < CH; ++k)
         x[k] = e0 + k < m8 ? nmc_ldv<NMC_SRC_SC1>(src + (size_t)(a + e0 + k) * C) : 0.0;
 #pragma unroll
-      for (int k = 0; k < 64; ++k)
+      for (int k = 0; k < CH; ++k)
         if (e0 + k < m8) r[k & 7] = e0 + k < 8 ? tr(x[k]) : r[k & 7] + tr(x[k]);
     }
     double res = m8 ? ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7])) : 0.0;

@@ -260,6 +260,8 @@ static size_t cnt_bytes(const nmc_ctx* x) {
 // plain load after a synchronize -- no device-to-host copy on every synchronize.
 // owner hand-off hyper-ready counters [RB <= ceil(C / 32)][P][32]
 static size_t hrd_words(const nmc_ctx* x) { return (size_t)32 * ((x->C + 31) / 32) * x->P; }
+// Dev.gsep role words [RB <= ceil(C / 32)][16] (u64, one 128-B line per chain block)
+static size_t grole_words(const nmc_ctx* x) { return (size_t)16 * ((x->C + 31) / 32); }
 
 static int check_timeout(nmc_ctx* x) {
   if (*x->tmo_host)
@@ -402,6 +404,9 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   // [RB][P][8 shards][32], RB <= ceil(C / 32)
   rc |= dalloc(x, &d.cnt, cnt_bytes(x) / sizeof(unsigned));
   rc |= dalloc(x, &d.hrd, hrd_words(x));
+  // Dev.gsep role words [RB <= ceil(C / 32)][16] and the fallback count
+  rc |= dalloc(x, &d.grole, grole_words(x));
+  rc |= dalloc(x, &d.gfb, 32);
   if (rc) { nmc_destroy(x); return rc; }
   {
     void* h = nullptr;
@@ -418,7 +423,16 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   }
   HIPCHK(hipMemset(d.cnt, 0, cnt_bytes(x)));
   HIPCHK(hipMemset(d.hrd, 0, hrd_words(x) * sizeof(unsigned)));
+  HIPCHK(hipMemset(d.grole, 0, grole_words(x) * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(d.gfb, 0, 32 * sizeof(unsigned)));
   d.pbase = d.xbase = 0;
+  // Dev.gsep: how long the two kernels may take to meet before the likelihood workgroups take
+  // a launch's Gibbs tasks over (NMC_GSEP_PATIENCE_US, default 2 ms); NMC_GSEP_SERIAL (tests)
+  // serializes them on one stream
+  d.gep = 0;
+  d.gpat = 200000u;
+  if (const char* e = getenv("NMC_GSEP_PATIENCE_US")) d.gpat = (unsigned)(atol(e) * 100);
+  x->gserial = getenv("NMC_GSEP_SERIAL") ? atoi(getenv("NMC_GSEP_SERIAL")) : 0;
   d.leaf = dleaf;
   d.merge = dmerge;
   HIPCHK(hipMemcpy(dleaf, starts.data(), starts.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -949,6 +963,16 @@ int nmc_kernel_name(nmc_ctx* x, char* out, int cap) {
   return 0;
 }
 
+int nmc_gibbs_fallbacks(nmc_ctx* x, int64_t* out) {
+  if (!out) return fail(-1, "gibbs fallbacks: null output");
+  hipSetDevice(x->device);
+  HIPCHK(hipStreamSynchronize(x->stream));
+  unsigned n = 0;
+  HIPCHK(hipMemcpy(&n, x->d.gfb, sizeof(unsigned), hipMemcpyDeviceToHost));
+  *out = (int64_t)n;
+  return 0;
+}
+
 int nmc_variate_source(nmc_ctx* x, int* in_kernel) {
   if (!in_kernel) return fail(-1, "variate source: null output");
   *in_kernel = x->d.zin ? 1 : 0;
@@ -1132,6 +1156,7 @@ int nmc_write_ll_csvs(nmc_ctx* x, const char* dir, const int32_t* chain_ids, int
       std::string s;
       for (int k = tid; k < q.nc; k += T) {
         const int c = q.c0 + k;
+        if (chain_ids[c] < 0) continue;   // (no file: a rank's padding chain)
         char path[4096];
         snprintf(path, sizeof(path), "%slogLikelihood.%d.csv", dir, chain_ids[c]);
         FILE* f = fopen(path, q.r0 == 0 ? "w" : "a");

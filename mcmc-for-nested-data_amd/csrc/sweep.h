@@ -289,6 +289,153 @@ __device__ __forceinline__ void nmc_hyper_once(const Dev& d, const double* src, 
   }
 }
 
+// ---- Dev.gsep without co-scheduling ----
+// The two kernels of the gsep path each wait on counters only the other advances, and HIP
+// does not promise that kernels on two streams run at the same time (a profiler's PMC pass,
+// AMD_SERIALIZE_KERNEL or a shared hardware queue serialize them).  So each chain block of a
+// launch has a role word (Dev.grole, epoch = Dev.gep): a Gibbs workgroup marks itself
+// started once its first task's values are published; if no Gibbs workgroup of the chain
+// block has started within Dev.gpat ticks, whichever side notices first sets the fallback
+// bit.  Then the Gibbs workgroups leave, and the likelihood workgroups' Gibbs waves update
+// every task of the launch themselves (nmc_hyper_update_stream: the same sums, draws and
+// outputs, so the same bits), group 0's writing and counting them as the Gibbs workgroup
+// would.  Either every task of a (launch, chain block) comes from the Gibbs kernel or every
+// one from the fallback: the bit is only set while no Gibbs workgroup has started.
+__device__ __forceinline__ unsigned long long* nmc_grole(const Dev& d, int cb) {
+  return d.grole + (size_t)cb * 16;
+}
+__device__ __forceinline__ bool nmc_grole_is_fallback(const Dev& d, unsigned long long v) {
+  return (unsigned)(v >> 32) == d.gep && (v & 1ull);
+}
+// (one lane) set the fallback bit of this launch; false: a Gibbs workgroup has started
+__device__ __forceinline__ bool nmc_grole_fallback(const Dev& d, int cb) {
+  unsigned long long* r = nmc_grole(d, cb);
+  const unsigned long long ep = (unsigned long long)d.gep << 32;
+  unsigned long long v = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if ((unsigned)(v >> 32) == d.gep) {
+      if (v & 1ull) return true;
+      if (v != ep) return false;   // started
+    }
+    if (__hip_atomic_compare_exchange_strong(r, &v, ep | 1ull, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      __hip_atomic_fetch_add(d.gfb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    }
+  }
+}
+// (one lane) a Gibbs workgroup starts its first task; false: the fallback is set, leave
+__device__ __forceinline__ bool nmc_grole_start(const Dev& d, int cb) {
+  unsigned long long* r = nmc_grole(d, cb);
+  const unsigned long long ep = (unsigned long long)d.gep << 32;
+  unsigned long long v = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    unsigned long long nv = ep + 2ull;
+    if ((unsigned)(v >> 32) == d.gep) {
+      if (v & 1ull) return false;
+      nv = v + 2ull;
+    }
+    if (__hip_atomic_compare_exchange_strong(r, &v, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      return true;
+  }
+}
+// The calling wave's patience clock (s_memrealtime: 100 MHz, one clock for the chip).
+__device__ __forceinline__ bool nmc_grole_patience_over(const Dev& d, unsigned long long t0) {
+  return __builtin_amdgcn_s_memrealtime() - t0 > (unsigned long long)d.gpat;
+}
+// A Gibbs workgroup's wait for its FIRST task's publications (wave 0; wave-uniform result):
+// 1 go on (started), 0 leave (the fallback is set, or a timeout recorded in d.tmo).
+__device__ __forceinline__ int nmc_grole_first_wait(const Dev& d, int cb, int q, unsigned target) {
+  const int lane = threadIdx.x & 63;
+  target += (unsigned)d.G * d.pbase;
+  unsigned* ctr = nmc_counter(d, cb, q, lane & 7);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool patient = true;
+  for (unsigned spins = 0;; ++spins) {
+    const unsigned v =
+        lane < 8 ? __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    unsigned tot = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tot += __builtin_amdgcn_readlane(v, k);
+    if (tot >= target) {
+      const bool go = lane == 0 ? nmc_grole_start(d, cb) : false;
+      return __builtin_amdgcn_readlane((int)go, 0);
+    }
+    if ((spins & 63) == 63) {
+      const unsigned long long rv =
+          __hip_atomic_load(nmc_grole(d, cb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (nmc_grole_is_fallback(d, rv)) return 0;
+      if (patient && nmc_grole_patience_over(d, t0)) {
+        const bool fb = lane == 0 ? nmc_grole_fallback(d, cb) : false;
+        if (__builtin_amdgcn_readlane((int)fb, 0)) return 0;
+        patient = false;   // a sibling has started: the likelihood kernel runs, wait for it
+      }
+    }
+    if ((spins & 255) == 255 &&
+        __hip_atomic_load(d.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+      return 0;
+    if (spins >= NMC_SPIN_LIMIT) {
+      __hip_atomic_store(d.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return 0;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+// A likelihood workgroup's Gibbs wave waiting for task (cb, q)'s ready count (wave-uniform):
+// 1 ready, -1 fallback (update it here), 0 timeout (d.tmo).
+__device__ __forceinline__ int nmc_grole_own_wait(const Dev& d, int cb, int q, unsigned target) {
+  const int lane = threadIdx.x & 63;
+  const unsigned* ctr = nmc_hrd(d, cb, q);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool patient = true;
+  for (unsigned spins = 0;; ++spins) {
+    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return 1;
+    if ((spins & 63) == 63) {
+      const unsigned long long rv =
+          __hip_atomic_load(nmc_grole(d, cb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (nmc_grole_is_fallback(d, rv)) return -1;
+      if (patient && nmc_grole_patience_over(d, t0)) {
+        const bool fb = lane == 0 ? nmc_grole_fallback(d, cb) : false;
+        if (__builtin_amdgcn_readlane((int)fb, 0)) return -1;
+        patient = false;   // a Gibbs workgroup has started: wait as long as it takes
+      }
+    }
+    if ((spins & 255) == 255 &&
+        __hip_atomic_load(d.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+      return 0;
+    if (spins >= NMC_SPIN_LIMIT) {
+      __hip_atomic_store(d.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return 0;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+// The fallback's update of task (tq, q) by one wave: HyperParameter.update (:463-498) with
+// the values streamed from global memory (sc1) in 32-value chunks -- nmc_pairwise_stream,
+// the order of nmc_hyper / nmc_hyper_once -- and the task's variates from the fill's ring or
+// drawn here (Dev.zin).  write: the global slot of tq and the sample row (group 0's wave).
+__device__ __noinline__ void nmc_hyper_update_stream(const Dev& d, int cb, int tq, int q,
+                                                     int cc, double* lds, int hyp, bool write) {
+  const int lane = threadIdx.x & 63;
+  const int P = d.P, G = d.G, C = d.C;
+  const double* src = ((tq & 1) ? d.vb1 : d.vb0) + (size_t)q * G * C + cc;
+  nmc_d2 hv;
+  if (d.zin) {
+    hv = nmc_sweep_hyper_variate(d.rhz, d.rhu, d.replay_n, d.rng_mode, P, C,
+                                 (uint32_t)(d.chain_base + cc), d.seed, d.ha, d.hlga, tq, q, cc);
+  } else {
+    const size_t hvi = (((size_t)(tq - d.vbase) * P + q) * C + cc) * 2;
+    hv.a = d.vh[hvi];
+    hv.b = d.vh[hvi + 1];
+  }
+  const double sdm = sqrt(lds[(hyp + NMC_HY_S2 * P + q) * 64 + lane] / G);
+  const double tot = nmc_pairwise_stream<32>(d, src, false, 0.0);
+  const double mu = tot / G + sdm * hv.a;                        // mu ~ N(mean(x), sqrt(s2/G))
+  const double ss = nmc_pairwise_stream<32>(d, src, true, mu);
+  nmc_hyper_finish(d, cb, tq, q, lds, hyp, write, mu, ss, hv.b);
+}
+
 // SYNC_OWN's Gibbs workgroup kb = (chain block, parameter q), four waves: every task (t, q)
 // of the launch in order, once its publication is complete -- HyperParameter.update
 // (:463-498) computed once per chain block, written through and counted ready (nmc_hrd)
@@ -330,7 +477,18 @@ __device__ __forceinline__ void nmc_sweep_gibbs_wg(int kb, double* lds) {
   for (int t = i0; t < i1; ++t) {
     A = nmc_sweep_args_at<Fam>();
     NMC_GSTAMP(3);
-    if (!nmc_wait_published(d, hcb, q, (unsigned)d.G * (unsigned)(t - i0 + 1), lds, H)) break;
+    if (GW > 0 && t == i0) {   // (Dev.gsep: the first task starts this workgroup, or the
+                               //  likelihood workgroups have taken the launch over)
+      if (threadIdx.x < 64) {
+        const int r = nmc_grole_first_wait(d, hcb, q, (unsigned)d.G);
+        if (threadIdx.x == 0) lds[H.flag * 64] = r ? 1.0 : 0.0;
+      }
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lds[H.flag * 64] == 0.0) break;
+    } else if (!nmc_wait_published(d, hcb, q, (unsigned)d.G * (unsigned)(t - i0 + 1), lds, H)) {
+      break;
+    }
     NMC_GSTAMP(0);
     if (w == 0) {   // the task's variates and sqrt(s2 / G) of the previous update
       nmc_d2 hv;
@@ -689,6 +847,7 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
   // ---- the Gibbs wave: its own loop, meeting the others at both barriers of every step ----
   if constexpr (PARTIAL) if (gw) {
     if (!(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
+    bool gfall = false;   // (SYNC_OWN, Dev.gsep: this launch's tasks are updated here)
     // task k = (kt, kq): poll its publication, update (HyperParameter.update :463-498),
     // write (the global slot of kt and the sample row); priors: this step's priors from the
     // update (p, sp, t: the step); returns the poll's verdict
@@ -697,15 +856,32 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
       const nmc_sweep_layout& L = v.L;
       const int kq = k % P, kt = k / P;
       if constexpr (OWN) {   // the Gibbs workgroup of (cb, kq) has counted task k ready
-        if (!nmc_poll_count(d, nmc_hrd(d, cb, kq), (unsigned)(kt - i0 + 1) + d.pbase))
-          return false;
+        const unsigned target = (unsigned)(kt - i0 + 1) + d.pbase;
+        if (!d.gsep) {
+          if (!nmc_poll_count(d, nmc_hrd(d, cb, kq), target)) return false;
+        } else if (!gfall) {   // (its own kernel: or nobody has started it, nmc_grole_*)
+          const int r = nmc_grole_own_wait(d, cb, kq, target);
+          if (r == 0) return false;
+          gfall = r < 0;
+        }
+        if (gfall) {   // the fallback: this wave updates task k (group 0's writes, counts it)
+          if (!nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1))) return false;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          nmc_hyper_update_stream(d, cb, kt, kq, cc, lds, L.hyp, write);
+          if (write) {
+            nmc_drain_vm();   // (stored before counted, as the Gibbs workgroup does)
+            if (lane == 0)
+              __hip_atomic_fetch_add(nmc_hrd(d, cb, kq), 1u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
       } else {
         if (!nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1))) return false;
       }
       // keep the payload loads below the poll (no instruction: wavefront scope)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if constexpr (OWN) {
-        nmc_hyper_read(d, kt, kq, cc, lds, L.hyp);
+        if (!gfall) nmc_hyper_read(d, kt, kq, cc, lds, L.hyp);
       } else {
         nmc_d2 hv;
         if (d.zin) {
@@ -786,6 +962,13 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
                              (unsigned)v.G * (unsigned)(close_k / v.P - i0 + 1), lds,
                              hl_view(v.L)))
         task(v, close_k, true, false, 0, 0, 0);
+    }
+    // SYNC_OWN, Dev.gsep: group 0's wave sees the launch's last tasks done -- by the Gibbs
+    // kernel (ready counts), or by itself when nobody started them (the fallback; also when
+    // the launch is too short for any task to fall due in the loop)
+    if constexpr (OWN) if (ok && d.gsep && g0w) {
+      for (int k = v.ge - v.lag > v.gs0 ? v.ge - v.lag : v.gs0; k < v.ge && ok; ++k)
+        ok = task(v, k, true, false, 0, 0, 0);
     }
     nmc_drain_vm();
     return;

@@ -43,12 +43,26 @@ static int nmc_sweep_call_t(nmc_ctx* x, const Fam& fam, NmcCall& c) {
         if (mode == NMC_MODE_SYNC_OWN && d.gsep) {
           // the Gibbs workgroups' kernel on the second stream, forked after the work before
           // this launch and joined before the work after it; both kernels resident together
-          // (NMC_OP_CAN_PERSIST), each spinning only on counters the other advances
+          // (NMC_OP_CAN_PERSIST), each waiting on counters the other advances -- and, when
+          // the two do not run at the same time after all, the likelihood workgroups take
+          // the launch's Gibbs tasks over (Dev.grole, this launch's epoch gep)
+          if (++x->gepoch == 0) ++x->gepoch;   // (0: a role word never written)
+          a.d.gep = x->gepoch;
+          const unsigned nb = grid.x / (unsigned)d.G;   // chain blocks of this launch
+          auto gibbs = [&](hipStream_t s) {
+            hipLaunchKernel(nmc_sweep_gibbs_kernel<Fam>(d.gwaves), dim3(nb * d.P),
+                            dim3(64 * d.gwaves), args, sweep_gibbs_lds_bytes(x), s);
+          };
+          if (x->gserial) {   // (tests: both kernels on one stream, serialized; 1: the Gibbs
+                              //  kernel first, 2: after the likelihood kernel)
+            if (x->gserial == 1) gibbs(x->stream);
+            hipLaunchKernel(nmc_sweep_kernel<Fam>(mode), grid, block, args, lds, x->stream);
+            if (x->gserial == 2) gibbs(x->stream);
+            return;
+          }
           hipEventRecord(x->gev[0], x->stream);
           hipStreamWaitEvent(x->gstream, x->gev[0], 0);
-          const unsigned nb = grid.x / (unsigned)d.G;   // chain blocks of this launch
-          hipLaunchKernel(nmc_sweep_gibbs_kernel<Fam>(d.gwaves), dim3(nb * d.P),
-                          dim3(64 * d.gwaves), args, sweep_gibbs_lds_bytes(x), x->gstream);
+          gibbs(x->gstream);
           hipLaunchKernel(nmc_sweep_kernel<Fam>(mode), grid, block, args, lds, x->stream);
           hipEventRecord(x->gev[1], x->gstream);
           hipStreamWaitEvent(x->stream, x->gev[1], 0);

@@ -67,6 +67,7 @@ SIGNATURES = {
     "nmc_kernel_name": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int]),
     "nmc_split_config": (ctypes.c_int, [_vp, _c_int_p, _c_int_p]),
     "nmc_variate_source": (ctypes.c_int, [_vp, _c_int_p]),
+    "nmc_gibbs_fallbacks": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64)]),
     "nmc_variogram": (ctypes.c_int, [ctypes.c_int, _c_double_p, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, _c_double_p]),
     "nmc_user_family_compile": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int,

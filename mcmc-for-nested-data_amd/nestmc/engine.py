@@ -213,6 +213,13 @@ class Engine:
         return dict(step_ms=sm.value, step_launches=sn.value, step_iters=si.value,
                     hyper_ms=hm.value, hyper_launches=hn.value)
 
+    def gibbs_fallbacks(self):
+        """(launch, chain block) pairs whose Gibbs tasks the step kernel updated itself
+        because the separate Gibbs kernel did not run beside it (nmc_gibbs_fallbacks)."""
+        n = ctypes.c_int64()
+        check(self.lib.nmc_gibbs_fallbacks(self.h, ctypes.byref(n)))
+        return n.value
+
     def launch_config(self):
         w, cb, pe, cl, md = (ctypes.c_int() for _ in range(5))
         check(self.lib.nmc_launch_config(self.h, ctypes.byref(w), ctypes.byref(cb),

@@ -60,13 +60,20 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
                      priorDistribution=None, startWithMLE=False, startingPointValueRange=None,
                      nProcesses=1, displayProgress=True, loggingLevel="info", *,
                      seed=0, devices=None, rng="philox", chains=None, return_samples=False,
-                     write_files=True, replay=None):
+                     write_files=True, replay=None, process_per_device=False, _rank=None):
     """Drop-in for posteriorSampling.samplePosterior (same positional/keyword API).
 
     Extra keyword-only options (all optional):
       seed       Philox seed (key = (global chain id, seed)); default 0
       devices    GPU ids to shard chains over (default: [0]); chains are split in
                  contiguous blocks so chain c always draws the same stream
+      process_per_device  one process per GPU instead of one engine per GPU in this
+                 process: this process starts len(devices) ranks (nestmc.ranks) before it
+                 makes any HIP call; rank r runs its contiguous block of chains on
+                 devices[r], and after the loop ONE RCCL gather brings every rank's sample
+                 store to rank 0, which writes every sample file (the reference's process
+                 fan-out, posteriorSampling.py:182-201, at the GPU level); the files are
+                 byte-identical to the one-process path's
       rng        "philox" (default) or "replay" (test use)
       replay     rng="replay": dict of captured variates z, u [C, iter, P, G] and
                  hz, hu [C, iter, P] (chain axis = position in ``chains``)
@@ -96,8 +103,14 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
     if nProcesses is None or nProcesses <= 0:
         nProcesses = os.cpu_count() or 1
     threads = max(1, min(int(nProcesses), 64))
-
-    if write_files:
+    if _rank is not None:
+        # a rank of process_per_device: the parent prepared the directories and logs the run
+        hg, world, rank = _rank
+        displayProgress = displayProgress and rank == 0
+        sample_dir = outputDirectory + "/sample/" if write_files else None
+        log_dir = outputDirectory + "/log/" if write_files else None
+        logger = None
+    elif write_files:
         sample_dir, log_dir = output.prepare_directories(outputDirectory)
         logger = output.get_logger(log_dir + "samplePosterior.log", "samplePosterior",
                                    loggingLevel)
@@ -131,17 +144,45 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
     chain_ids = list(range(nChains)) if chains is None else [int(c) for c in chains]
     if (rng == "replay") != (replay is not None):
         raise ValueError("rng='replay' needs replay= variates (and only then)")
+    devices = [0] if devices is None else list(devices)
+    if process_per_device and _rank is None:
+        # one process per GPU, started before this process makes any HIP call
+        if chains is not None or replay is not None:
+            raise ValueError("process_per_device runs all nChains chains on the Philox "
+                             "stream (no chains= / replay=)")
+        from . import ranks
+        kw = dict(nChains=nChains, nIter=nIter, nSamples=nSamples, parameterName=names,
+                  nGroups=nGroups, nResponsesPerGroup=nResponsesPerGroup, pooling=pooling,
+                  logLikelihoodFunction=logLikelihoodFunction, outputDirectory=outputDirectory,
+                  saveLogLikelihood=saveLogLikelihood, priorDistribution=priorDistribution,
+                  startWithMLE=startWithMLE, startingPointValueRange=startingPointValueRange,
+                  nProcesses=max(1, threads // len(devices)), displayProgress=displayProgress,
+                  loggingLevel=loggingLevel, seed=seed, rng=rng,
+                  return_samples=return_samples, write_files=write_files)
+        res = ranks.run_per_device(kw, devices)
+        _finish_log(logger, [], start_time, displayProgress)
+        return res
     if _lib.device_count() < 1:
         raise _lib.NestmcError("no HIP device visible: the sampler runs on MI355X only")
-    devices = [0] if devices is None else list(devices)
+    rank_info = None
+    if _rank is not None:
+        # this rank's padded contiguous shard (equal store sizes for the RCCL gather; chains
+        # with ids >= nChains are padding, run and dropped) on its own device
+        from .parallel import padded_shard
+        s0, per, real = padded_shard(nChains, world, rank)
+        chain_ids = list(range(s0, s0 + per))
+        rank_info = dict(hg=hg, world=world, rank=rank, device=devices[rank], n_total=nChains)
+        devices = [devices[rank]]
     partial = pooling == "partial"
 
     # ---- chain logs; initialisation (reference RNG order, RandomState(chain)) ----
     if displayProgress:
         output.print_progress("Initialising %d chains." % len(chain_ids))
     chain_logs = []
-    if logger:
+    if log_dir:
         for c in chain_ids:
+            if c >= nChains:        # (a rank's padding chains)
+                continue
             lg = output.get_logger(log_dir + "/mcmc.chain%.2i.log" % c, "mcmc.chain%.2i" % c,
                                    loggingLevel)
             lg.info("chain %i. Started looking for a reasonable starting state." % c)
@@ -194,17 +235,57 @@ def sample_posterior(nChains, nIter, nSamples, parameterName, nGroups, nResponse
     try:
         return _sample_loop(engines, nIter, burn, thin, names, G, partial, saveLogLikelihood,
                             write_files, sample_dir, threads, displayProgress, return_samples,
-                            logger, chain_logs, start_time)
+                            logger, chain_logs, start_time, rank_info)
     finally:
         for eng, _, _ in engines:
             eng.close()
 
 
+def _finish_log(logger, chain_logs, start_time, displayProgress):
+    elapsed = datetime.datetime.now() - start_time
+    msg = "Finished. The elapsed time in total is %s." \
+        % datetime.timedelta(seconds=int(elapsed.total_seconds()))
+    for lg in chain_logs:
+        lg.info("100% complete.")
+        output.close_logger(lg)
+    if logger:
+        logger.info(msg)
+        output.close_logger(logger)
+    if displayProgress:
+        print("")
+        output.print_progress(msg)
+
+
+def _gather_rank(engines, rank_info):
+    """process_per_device: ONE ncclGather of every rank's sample store to rank 0 (RCCL over
+    xGMI), the padding chains dropped -> rank 0: [rows][cols][nChains], others: None; the
+    accepted counts travel over the host group (rank 0: [nChains, P, G])."""
+    from . import parallel
+    eng = engines[0][0]
+    hg, world, rank, n = (rank_info[k] for k in ("hg", "world", "rank", "n_total"))
+    comm = parallel.rccl_comm(hg, world, rank, rank_info["device"])
+    try:
+        full = parallel.gather_samples(eng, comm, root=0)
+    finally:
+        parallel.rccl_destroy(comm)
+    reals = [parallel.padded_shard(n, world, r)[2] for r in range(world)]
+    acc = hg.gather(numpy.ascontiguousarray(eng.accept_counts()).tobytes())
+    if rank != 0:
+        return None, None
+    raw = parallel.assemble(full, reals)
+    P, G = eng.P, eng.G
+    accs = [numpy.frombuffer(a, dtype=numpy.int64).reshape(-1, P, G)[:reals[r]]
+            for r, a in enumerate(acc)]
+    return raw, numpy.concatenate(accs, axis=0)
+
+
 def _sample_loop(engines, nIter, burn, thin, names, G, partial, saveLogLikelihood, write_files,
                  sample_dir, threads, displayProgress, return_samples, logger, chain_logs,
-                 start_time):
+                 start_time, rank_info=None):
     """The device loop, the per-observation LL rows and the sample files of
-    sample_posterior (the caller closes the engines whatever happens here)."""
+    sample_posterior (the caller closes the engines whatever happens here).  rank_info: a
+    rank of process_per_device -- this rank writes its chains' logLikelihood files, rank 0
+    every sample file after the gather."""
     # ---- the device loop ----------------------------------------------------
     rec = record_iterations(nIter, burn, thin)
     if displayProgress:
@@ -222,37 +303,41 @@ def _sample_loop(engines, nIter, burn, thin, names, G, partial, saveLogLikelihoo
     for eng, _, _ in engines:
         eng.synchronize()
     loop_seconds = (datetime.datetime.now() - t_loop).total_seconds()
+    n_total = None if rank_info is None else rank_info["n_total"]
     if saveLogLikelihood and write_files:
         # every recorded row's per-observation LL (:890-891, :907-909 at the values of
         # :656-659), re-evaluated on the device from the sample store and streamed out
+        # (a rank's padding chains: file id -1, no file)
         for eng, _, ids in engines:
-            eng.write_ll_csvs(sample_dir, ids, threads=threads)
+            fids = ids if n_total is None else [c if c < n_total else -1 for c in ids]
+            eng.write_ll_csvs(sample_dir, fids, threads=threads)
 
     # ---- samples -> files ----------------------------------------------------
     header = output.header_names(names, G, partial)
+    hdr = header if burn < nIter else None
     rows_all = []
-    for eng, s0, ids in engines:
-        raw = eng.samples_raw()                     # [rows][cols][C_local]
-        if write_files:
-            hdr = header if burn < nIter else None
-            output.write_sample_csvs(sample_dir, raw, list(range(len(ids))), ids, hdr, rec,
-                                     threads=threads)
-        if return_samples:
+    if rank_info is not None:
+        raw, accept = _gather_rank(engines, rank_info)
+        if raw is not None:
+            if write_files:
+                ids = list(range(n_total))
+                output.write_sample_csvs(sample_dir, raw, ids, ids, hdr, rec, threads=threads)
             rows_all.append(numpy.transpose(raw, (2, 0, 1)))
-    accept = [eng.accept_counts() for eng, _, _ in engines] if return_samples else None
+        accept = [accept] if accept is not None else []
+    else:
+        for eng, s0, ids in engines:
+            raw = eng.samples_raw()                     # [rows][cols][C_local]
+            if write_files:
+                output.write_sample_csvs(sample_dir, raw, list(range(len(ids))), ids, hdr, rec,
+                                         threads=threads)
+            if return_samples:
+                rows_all.append(numpy.transpose(raw, (2, 0, 1)))
+        accept = [eng.accept_counts() for eng, _, _ in engines] if return_samples else None
 
-    elapsed = datetime.datetime.now() - start_time
-    msg = "Finished. The elapsed time in total is %s." \
-        % datetime.timedelta(seconds=int(elapsed.total_seconds()))
-    if logger:
-        for lg in chain_logs:
-            lg.info("100% complete.")
-            output.close_logger(lg)
-        logger.info(msg)
-        output.close_logger(logger)
-    if displayProgress:
-        print("")
-        output.print_progress(msg)
+    # (a rank: the parent prints and logs the end of the run)
+    _finish_log(logger, chain_logs, start_time, displayProgress and rank_info is None)
+    if rank_info is not None and rank_info["rank"] != 0:
+        return None
     if return_samples:
         return {"rows": numpy.concatenate(rows_all, axis=0), "row_index": rec,
                 "header": header, "burn": burn, "thin": thin,

@@ -118,6 +118,7 @@ def run_engine(fam, sizes, st, sel, chain_base, n_iter, seed, pooling="partial",
     acc, llp = eng.trace(n_iter)
     rows = eng.samples()
     cfg = eng.launch_config()
+    cfg["gibbs_fallbacks"] = eng.gibbs_fallbacks()
     eng.close()
     return acc, llp, rows, cfg
 

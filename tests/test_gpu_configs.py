@@ -60,6 +60,38 @@ def test_cfg4_sweep_resident_batches_of_chain_blocks(gpu_lib):
         assert numpy.array_equal(bat[k], ref[k], equal_nan=True), k
 
 
+def test_cfg4_gsep_serialized_kernels_fall_back(gpu_lib):
+    """The cfg-4 shard (128 chains x 256 groups x 2000 rows) on its default path -- nmc_k_sweep
+    SYNC_OWN beside its Gibbs kernel nmc_k_sweep_gibbs on a second stream -- when the two
+    kernels do NOT run at the same time (as under a profiler's PMC pass): both on one stream,
+    the Gibbs kernel first (it gives up after the patience and leaves) or second (it finds the
+    launch taken over and leaves).  Every launch completes, the likelihood workgroups update
+    the Gibbs tasks themselves, and flags, proposal LLs and recorded rows (hyper-parameters
+    included) are bit for bit nmc_k_run's, over launches of 2, 2 and 1 iterations (the last
+    one too short for any task to fall due inside its loop)."""
+    G, N, n_iter, seed, C = 256, 2000, 5, 43, 128
+    x, y, _, _ = data.linreg(G, N, seed=7)
+    fam = LinearRegression.simple(x, y, sigma=1.0)
+    sizes = [N] * G
+    st, _ = partial_state(fam, sizes, C, 2)
+    sel = numpy.arange(C)
+    ref = run_engine(fam, sizes, st, sel, 0, n_iter, seed, launch_iters=2,
+                     env={"NMC_SWEEP": "0"})
+    assert ref[3]["kernel"].startswith("nmc_k_run<"), ref[3]
+    sep = run_engine(fam, sizes, st, sel, 0, n_iter, seed, launch_iters=2)
+    assert sep[3]["kernel"].startswith("nmc_k_sweep<") and sep[3]["mode"] == "NMC_MODE_SYNC_OWN"
+    assert sep[3]["gibbs_fallbacks"] == 0, sep[3]   # (the two kernels met)
+    runs = {"sep": sep}
+    for order in ("1", "2"):
+        runs[order] = run_engine(fam, sizes, st, sel, 0, n_iter, seed, launch_iters=2,
+                                 env={"NMC_GSEP_SERIAL": order, "NMC_GSEP_PATIENCE_US": "500"})
+        # every (launch, chain block) fell back: 3 launches x 2 chain blocks
+        assert runs[order][3]["gibbs_fallbacks"] == 6, (order, runs[order][3])
+    for name, r in runs.items():
+        for k in range(3):
+            assert numpy.array_equal(r[k], ref[k], equal_nan=True), (name, k)
+
+
 @pytest.mark.parametrize("G", [129, 256])
 def test_cfg4_geometry_multileaf_gibbs(gpu_lib, G):
     N, n_iter, seed = 2000, 8, 31

@@ -89,6 +89,32 @@ def test_devices_replay_writes_reference_csvs(gpu_lib, tmp_path, name):
         assert filecmp.cmp(mine, c.csv_path(ch), shallow=False), (name, ch)
 
 
+def test_process_per_device_one_rank_byte_identical(gpu_lib, tmp_path):
+    """samplePosterior(process_per_device=True): this process starts one rank per device
+    (nestmc.ranks) before touching the GPU; the rank samples its chains, gathers its sample
+    store to rank 0 with ncclGather and writes every file -- byte for byte the in-process
+    path's files (samples, per-observation LLs) and the same returned arrays."""
+    C, G, N = 70, 6, 40
+    fam, sizes, priors, pooling, names = synthetic("linreg_partial", C, G, N)
+    kw = dict(saveLogLikelihood=True, priorDistribution=priors,
+              startingPointValueRange={n: [-0.5, 0.5] for n in names}, displayProgress=False,
+              seed=23)
+    one, ppd = str(tmp_path / "one"), str(tmp_path / "ppd")
+    r1 = sample_posterior(C, 60, 20, names, G, N, pooling, fam, one, devices=[0],
+                          return_samples=True, **kw)
+    r2 = sample_posterior(C, 60, 20, names, G, N, pooling, fam, ppd, devices=[0],
+                          return_samples=True, process_per_device=True, **kw)
+    files = _files(one)
+    assert sum(f.startswith("sample.") for f in files) == C
+    assert _files(ppd) == files
+    _same_tree(one, ppd, files)
+    assert sorted(os.listdir(os.path.join(ppd, "log"))) == \
+        sorted(os.listdir(os.path.join(one, "log")))
+    assert numpy.array_equal(r1["rows"], r2["rows"], equal_nan=True)
+    assert numpy.array_equal(r1["accepted"], r2["accepted"])
+    assert r1["row_index"] == r2["row_index"]
+
+
 # ---- two processes (host-group ranks), each driving its own engine on the GPU ----------
 def _npy(*arrays):
     import io
