@@ -15,8 +15,6 @@
 
 #include "../../include/nestmc.h"
 #include "kernels.h"
-#include "duo.h"
-#include "step.h"
 #include "sweep.h"
 
 // error message of the calling thread (nestmc.hip); returns code
@@ -67,11 +65,8 @@ struct nmc_ctx {
   volatile unsigned* tmo_host = nullptr;  // host view of d.tmo (coherent pinned memory)
   void* user = nullptr;                   // user family: its per-device kernel table (user.hip)
   double* user_k = nullptr;               // user family: device copy of the model constants
-  bool step_ok = false;                   // nmc_k_step where it applies (NMC_STEP=1)
   bool sweep = false;                     // nmc_k_sweep runs the loop (choose_geometry)
   bool no_sweep = false;                  // (its grid could not be resident: nmc_k_run)
-  bool duo = false;                       // nmc_k_duo runs the loop (choose_geometry)
-  bool no_duo = false;                    // (its grid could not be resident: nmc_k_run)
 };
 
 static inline double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->d.vb0; }
@@ -86,26 +81,12 @@ static inline size_t lds_bytes_for(const nmc_ctx* x, int hlds, int rows_lds) {
              .total * 512;
 }
 static inline int run_mode(const nmc_ctx* x) {
-  if (x->duo) return NMC_MODE_DUO;
   if (x->pooling != NMC_POOL_PARTIAL) return x->d.CL == 32 ? NMC_MODE_HALF : NMC_MODE_NOPOOL;
   if (x->sweep)
     return x->d.G <= 64 ? NMC_MODE_SYNC_REG : x->d.G <= 128 ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC_OWN;
   if (!x->persistent) return NMC_MODE_LAUNCH;
-  if (x->d.hreg) return x->d.hown ? NMC_MODE_SYNC_OWN : NMC_MODE_SYNC_REG;
+  if (x->d.hreg) return NMC_MODE_SYNC_REG;
   return x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
-}
-
-// The one-barrier step kernel (step.h) runs mode `mode` when the groups' rows are in LDS,
-// there is no row split, and the mode is none/complete pooling or the register hand-off of
-// at most 64 groups (one 64-value fetch per Gibbs task).
-static inline bool uses_step(const nmc_ctx* x, int mode) {
-  return x->step_ok && x->d.rows_lds && x->d.S == 1 &&
-         (mode == NMC_MODE_NOPOOL ||
-          (mode == NMC_MODE_SYNC_REG && x->d.W >= 3 && x->d.G <= 64));
-}
-static inline size_t step_lds_bytes(const nmc_ctx* x) {
-  return (size_t)nmc_step_lds(x->nacc, x->d.P, x->pooling == NMC_POOL_PARTIAL,
-                              x->d.nmax * x->nf, x->d.G).total * 512;
 }
 
 // LDS of nmc_k_sweep (sweep.h); partial pooling over G > 128 groups also runs the Gibbs
@@ -131,15 +112,8 @@ static inline int64_t sweep_grid(const nmc_ctx* x) {
          (x->pooling == NMC_POOL_PARTIAL && d.G > 128 && !d.gsep ? (int64_t)d.RB * d.P : 0);
 }
 
-// LDS of nmc_k_duo (duo.h): both half blocks' state, the control words and the group's rows
-static inline size_t duo_lds_bytes(const nmc_ctx* x) {
-  return (size_t)nmc_duo_lds(x->d.P, (int)(x->d.nmax * x->nf)).total * 8;
-}
-
 static inline size_t run_lds_bytes(const nmc_ctx* x) {
-  if (x->duo) return duo_lds_bytes(x);
   if (x->sweep) return sweep_lds_bytes(x);
-  if (uses_step(x, run_mode(x))) return step_lds_bytes(x);
   return lds_bytes_for(x, x->persistent && x->d.hlds ? 1 : 0, x->d.rows_lds);
 }
 
@@ -154,15 +128,12 @@ static inline int nmc_safe_blocks(const nmc_ctx* x, int nb) {
 }
 // mode of the persistent partial-pooling kernel (its occupancy query)
 static inline int nmc_persist_mode(const nmc_ctx* x) {
-  if (x->sweep || x->duo) return run_mode(x);
-  return x->d.hreg ? (x->d.hown ? NMC_MODE_SYNC_OWN : NMC_MODE_SYNC_REG)
-                   : x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
+  if (x->sweep) return run_mode(x);
+  return x->d.hreg ? NMC_MODE_SYNC_REG : x->d.hlds ? NMC_MODE_SYNC_LDS : NMC_MODE_SYNC;
 }
 // LDS of the persistent partial-pooling kernel (its occupancy query)
 static inline size_t nmc_persist_lds(const nmc_ctx* x) {
-  if (x->duo) return duo_lds_bytes(x);
   if (x->sweep) return sweep_lds_bytes(x);
-  if (uses_step(x, nmc_persist_mode(x))) return step_lds_bytes(x);
   return lds_bytes_for(x, x->d.hlds && !x->d.hreg, x->d.rows_lds);
 }
 

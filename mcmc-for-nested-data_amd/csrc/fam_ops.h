@@ -13,7 +13,6 @@ static const void* nmc_run_kernel_rl(int mode) {
     case NMC_MODE_LAUNCH: return (const void*)nmc_k_run<Fam, NMC_MODE_LAUNCH, RL>;
     case NMC_MODE_SYNC: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC, RL>;
     case NMC_MODE_SYNC_REG: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_REG, RL>;
-    case NMC_MODE_SYNC_OWN: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_OWN, RL>;
     case NMC_MODE_HALF:   // (rows in LDS, row pairs in every block: the host's condition)
       if constexpr (RL && nmc_paired_rows_ok<Fam>())
         return (const void*)nmc_k_run<Fam, NMC_MODE_HALF, true>;
@@ -23,13 +22,6 @@ static const void* nmc_run_kernel_rl(int mode) {
 }
 template <class Fam>
 static const void* nmc_run_kernel(const nmc_ctx* x, int mode) {
-  if (mode == NMC_MODE_DUO) {   // (the {x, y} regression rows only: the host's condition)
-    if constexpr (Fam::ASM_ROWS) return (const void*)nmc_k_duo<Fam>;
-    return nullptr;
-  }
-  if (uses_step(x, mode))
-    return mode == NMC_MODE_NOPOOL ? (const void*)nmc_k_step<Fam, NMC_MODE_NOPOOL>
-                                   : (const void*)nmc_k_step<Fam, NMC_MODE_SYNC_REG>;
   return x->d.rows_lds ? nmc_run_kernel_rl<Fam, true>(mode) : nmc_run_kernel_rl<Fam, false>(mode);
 }
 

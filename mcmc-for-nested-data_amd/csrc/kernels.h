@@ -91,16 +91,9 @@ struct Dev {
   int nmax;              // rows of the largest group
   int hlds, naux;        // persistent partial: Gibbs payload via LDS, auxiliary waves
   int hreg;              // persistent partial, G <= 64: Gibbs payload in registers (SYNC_REG)
-  // SYNC_REG with G > 64 ("owner" hand-off): the Gibbs update of task k (parameter k % P
-  // after iteration k / P) is computed once per chain block, by the Gibbs wave of the
-  // workgroup of group k % G (member 0), one step after its publication; it writes the
-  // hyper-parameters to the global slot and counts them on hrd[(cb * P + q) * 32]; every
-  // workgroup then reads the four values instead of streaming the G published values itself
-  int hown;
-  unsigned* hrd;         // [RB][P][32] hyper-ready counters (pbase tasks per parameter before)
+  unsigned* hrd;         // [RB][P][32] hyper-ready counts of nmc_k_sweep's Gibbs workgroups
+                         // (SYNC_OWN; pbase tasks per parameter before)
   int noprio;            // diagnostics: no issue priority for the latency-bound waves
-  int sflags;            // nmc_k_step variants (bit-identical; NMC_STEP_FLAGS): 1 Gibbs payload
-                         // via LDS-DMA, 2 next proposal formed before the barrier
   int pubearly;          // nmc_k_sweep: the control counts the previous step's publication
                          // before taking a tile (its store drained first), not after one
   int gwaves;            // waves of nmc_k_sweep_gibbs (4)
@@ -120,7 +113,6 @@ struct Dev {
                          // entries left (default), 2 like every other wave
   int gtiles;            // nmc_k_sweep, the Gibbs wave after its task (NMC_GIBBS_TILES): 0 no
                          // tiles, 1 as ctiles 1 (default)
-  int dkt;               // nmc_k_duo: likelihood tiles per ticket (NMC_DUO_KT)
   int rows_lds;          // 1: each workgroup stages its group's rows in LDS once per launch
   int tile;              // target rows per likelihood tile (nmc_tiles)
   unsigned* cnt;         // [CB][P][32] publish counters (persistent partial): zeroed at create,
@@ -633,9 +625,8 @@ __device__ __forceinline__ bool nmc_poll_published(const Dev& d, int cb, int p, 
   }
 }
 
-// Owner hand-off (Dev.hown): the workgroup whose Gibbs wave computes task k, and the
-// calling wave's bounded poll of a task counter (the hyper-ready count of (cb, q)).
-__device__ __forceinline__ int nmc_task_owner(const Dev& d, int k) { return k % d.G; }
+// The hyper-ready count of (cb, q) (nmc_k_sweep's Gibbs workgroups, SYNC_OWN) and the
+// calling wave's bounded poll of such a count.
 __device__ __forceinline__ unsigned* nmc_hrd(const Dev& d, int cb, int q) {
   return d.hrd + ((size_t)cb * d.P + q) * 32;
 }
@@ -1266,7 +1257,7 @@ __device__ __forceinline__ void nmc_hyper_compute(const Dev& d, int cb, int t, i
   hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
   if (write && nmc_lane_owns(d, c, lane)) {
     const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
-    // write-through (sc1): the owner hand-off's readers poll for them inside the launch
+    // write-through (sc1): nmc_k_sweep's readers poll for them inside the launch
     __hip_atomic_store(d.mu + ho, mu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(d.s2 + ho, s2n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(d.hsd + ho, sdn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1372,7 +1363,7 @@ __device__ __forceinline__ void nmc_hyper_finish(const Dev& d, int cb, int t, in
   hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sdn;
   if (write && nmc_lane_owns(d, c, lane)) {
     const size_t ho = nmc_hslot(d, t) + (size_t)p * C + c;
-    // write-through (sc1): the owner hand-off's readers poll for them inside the launch
+    // write-through (sc1): nmc_k_sweep's readers poll for them inside the launch
     __hip_atomic_store(d.mu + ho, mu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(d.s2 + ho, s2n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(d.hsd + ho, sdn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1510,7 +1501,7 @@ __device__ __forceinline__ double nmc_pairwise_stream(const Dev& d, const double
   return ls[0];
 }
 
-// Owner hand-off: the hyper-parameters of task (tq, q) as its owner stored them (global
+// SYNC_OWN: the hyper-parameters of task (tq, q) as its Gibbs workgroup stored them (global
 // slot of tq, sc1 loads) -> this workgroup's LDS hyper state (nmc_hyper_finish's values).
 __device__ __forceinline__ void nmc_hyper_read(const Dev& d, int tq, int q, int cc, double* lds,
                                                int hyp) {
@@ -1527,30 +1518,13 @@ __device__ __forceinline__ void nmc_hyper_read(const Dev& d, int tq, int q, int 
   hy[(NMC_HY_ISD * P + q) * 64] = 1.0 / sd;
 }
 
-// STREAM = false (the register mode's instance) compiles only the G <= 64 path: the
-// streamed passes' code cost the cfg-3 kernel 740 more SGPR spills (903 against 166).
-// The register Gibbs update of task (tq, q) for this wave's 64 chains: G <= 64 from one
-// 64-value fetch (nmc_hyper_fetch_reg / _compute_reg), 64 < G <= 256 streamed
-// (nmc_pairwise_stream, two passes).  Same sums, draws and outputs either way.
-template <bool STREAM>
+// The register Gibbs update of task (tq, q) for this wave's 64 chains (G <= 64): one
+// 64-value fetch (nmc_hyper_fetch_reg), then nmc_hyper_compute_reg.
 __device__ __forceinline__ void nmc_hyper_update_reg(const Dev& d, int cb, int tq, int q, int cc,
                                                      double* lds, int hyp, bool write) {
-  if (!STREAM || d.G <= 64) {
-    double xv[64], fz, fx;
-    nmc_hyper_fetch_reg(d, tq, q, cc, xv, fz, fx);
-    nmc_hyper_compute_reg(d, cb, tq, q, lds, hyp, write, fz, fx, xv);
-    return;
-  }
-  const int lane = threadIdx.x & 63;
-  const int P = d.P, G = d.G, C = d.C;
-  const double* src = ((tq & 1) ? d.vb1 : d.vb0) + (size_t)q * G * C + cc;
-  const size_t hvi = (((size_t)(tq - d.vbase) * P + q) * C + cc) * 2;
-  const double hz = d.vh[hvi], hx = d.vh[hvi + 1];
-  const double sdm = sqrt(lds[(hyp + NMC_HY_S2 * P + q) * 64 + lane] / G);
-  const double tot = nmc_pairwise_stream(d, src, false, 0.0);
-  const double mu = tot / G + sdm * hz;                        // mu ~ N(mean(x), sqrt(s2/G))
-  const double ss = nmc_pairwise_stream(d, src, true, mu);
-  nmc_hyper_finish(d, cb, tq, q, lds, hyp, write, mu, ss, hx);
+  double xv[64], fz, fx;
+  nmc_hyper_fetch_reg(d, tq, q, cc, xv, fz, fx);
+  nmc_hyper_compute_reg(d, cb, tq, q, lds, hyp, write, fz, fx, xv);
 }
 
 // ---------------------------------------------------------------------------
@@ -1582,7 +1556,7 @@ enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
        NMC_MODE_SYNC_LDS = 3,    // persistent, the Gibbs wave works on an LDS copy
        NMC_MODE_SYNC_REG = 4,    // persistent, G <= 64: the Gibbs wave fetches the task's
                                  // values straight into registers and updates in one step
-       NMC_MODE_SYNC_OWN = 5,    // persistent, G > 64, opt-in: the owner hand-off (Dev.hown)
+       NMC_MODE_SYNC_OWN = 5,    // nmc_k_sweep (G > 128): Gibbs workgroups update each task
        NMC_MODE_HALF = 6 };      // none/complete pooling, 32 chains per workgroup: lanes l
                                  // and l + 32 hold chain l, on the two row parities
 // RL: the groups' rows are staged in LDS for the launch (d.rows_lds) -- a template
@@ -1596,7 +1570,7 @@ enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
 typedef __attribute__((address_space(4))) const Dev* nmc_kdev_ptr;
 __device__ __forceinline__ const Dev* nmc_kdev() {
   nmc_kdev_ptr p = (nmc_kdev_ptr)__builtin_amdgcn_kernarg_segment_ptr();
-#if !defined(NMC_STAMPS) && !defined(NMC_NO_LAUNDER) && !defined(NMC_DUO_STAMPS)
+#if !defined(NMC_STAMPS) && !defined(NMC_NO_LAUNDER)
   // (the stamps build's divergent stamp stores make the backend move the laundered pointer
   //  to VGPRs, an illegal copy: diagnostics keep it plain; NMC_NO_LAUNDER: the A/B build)
   asm volatile("" : "+s"(p));
@@ -1632,11 +1606,10 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   const bool g0w = g == 0 && mb == 0;   // writes the chain block's hyper-parameters
   const int cc = c < C ? c : C - 1;
   constexpr bool sync = MODE == NMC_MODE_SYNC || MODE == NMC_MODE_SYNC_LDS ||
-                        MODE == NMC_MODE_SYNC_REG || MODE == NMC_MODE_SYNC_OWN;
-  // Gibbs-wave modes: payload in LDS (two-stage pipeline) or in registers (one stage; the
-  // owner hand-off is its own instance, so its code never costs the register mode)
-  constexpr bool own = MODE == NMC_MODE_SYNC_OWN;
-  constexpr bool hr = MODE == NMC_MODE_SYNC_REG || own;
+                        MODE == NMC_MODE_SYNC_REG;
+  static_assert(MODE != NMC_MODE_SYNC_OWN, "SYNC_OWN is nmc_k_sweep's mode");
+  // Gibbs-wave modes: payload in LDS (two-stage pipeline) or in registers (one stage)
+  constexpr bool hr = MODE == NMC_MODE_SYNC_REG;
   constexpr bool hl = MODE == NMC_MODE_SYNC_LDS || hr;
   // the Gibbs wave's task at global step gs is gs - lag; the register mode updates a
   // task two steps after its publication (P >= 2: the hand-off latency -- store drain,
@@ -1646,7 +1619,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   // register mode: the task this workgroup closes after the loop (-1: none)
   const int close_k = [&]() {
     const int ge = i1 * P, k0 = ge - lag > i0 * P ? ge - lag : i0 * P;
-    return hr && !own && mb == 0 && k0 + g < ge ? k0 + g : -1;
+    return hr && mb == 0 && k0 + g < ge ? k0 + g : -1;
   }();
   // rows in LDS for the launch, or every wave's two staging buffers (nmc_ll_rows_staged)
   const int row_doubles = RL ? d.nmax * Fam::NFIELDS
@@ -1855,81 +1828,9 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       kq = (int)__builtin_amdgcn_readlane(kn, 0);
     }
   };
-  // ---- register mode: the Gibbs wave runs its own loop, so its 64-value payload never
-  //      shares registers with the control code; after its update it takes likelihood
-  //      tiles like every other wave, and it meets them at the same two barriers ----
-  if constexpr (own) if (gw) {
-    // owner hand-off (G > 64): at step gs the wave (a) reads task gs - lag, computed by its
-    // owner, for this step's priors and (b) computes task gs - 1 when this workgroup owns
-    // it (needed at step gs - 1 + P); P == 1 needs task gs - 1 at once: (b) before (a)
-    const int gs0 = i0 * P;
-    const bool own = mb == 0;
-    auto owner_task = [&](int k) -> bool {   // poll the publication, update, count it
-      if (!own || k < gs0 || nmc_task_owner(d, k) != g) return true;
-      const int kq = k % P, kt = k / P;
-      if (!nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1))) return false;
-      // keep the payload loads below the poll (no instruction: wavefront scope)
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      nmc_hyper_update_reg<true>(d, cb, kt, kq, cc, lds, L.hyp, true);
-      nmc_drain_vm();   // the hyper-parameters are stored before they are counted
-      if (lane == 0)
-        __hip_atomic_fetch_add(nmc_hrd(d, cb, kq), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return true;
-    };
-    for (int t = i0; t < i1 && ok; ++t) {
-      for (int p = 0; p < P; ++p) {
-        dP = nmc_kdev();
-        const int gs = t * P + p;
-        const bool due = gs - lag >= gs0;
-        bool okw = P == 1 ? owner_task(gs - 1) : true;
-        if (due) {   // task k = gs - lag = (kt, kq): wait for its owner, read it
-          const int k = gs - lag, kq = k % P, kt = k / P;
-          const bool r = okw && nmc_poll_count(d, nmc_hrd(d, cb, kq), (unsigned)(kt - i0 + 1) + d.pbase);
-          if (lane == 0)
-            __hip_atomic_store(lds + L.flag * 64 + 1, r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (r) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            nmc_hyper_read(d, kt, kq, cc, lds, L.hyp);
-            if (P <= 2) {   // this step's priors from the update just read
-              const int sp = gs & 1;
-              const double v = th[p * 64];
-              const double prop = v + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
-                                          lds[(L.zl + 2 * sp) * 64 + 2 * lane];
-              const double m = hy[(NMC_HY_MU * P + p) * 64], sd = hy[(NMC_HY_SD * P + p) * 64];
-              const double lsd = hy[(NMC_HY_LSD * P + p) * 64], isd = hy[(NMC_HY_ISD * P + p) * 64];
-              cwv[NMC_CW_LPC * 64] =
-                  t > 0 ? nmc_norm_logpdf_r(v, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
-              cwv[NMC_CW_LPP * 64] = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
-            }
-          }
-        }
-        // (a failed owner poll has set the timeout word: the next due poll fails and every
-        // wave leaves at the same step)
-        if (P > 1) okw = owner_task(gs - 1);
-        (void)okw;
-        __syncthreads();   // A
-        if (due) {
-          ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
-          if (!ok) break;
-        }
-        __syncthreads();   // B
-      }
-    }
-    // closing: the last task's owner computes and counts it (the matching barrier of the
-    // other waves' nmc_wait_published); every earlier task was computed in the loop
-    if (ok && own && nmc_task_owner(d, i1 * P - 1) == g) {
-      if (nmc_wait_published(d, cb, P - 1, (unsigned)G * (unsigned)(i1 - i0), lds, L)) {
-        nmc_hyper_update_reg<true>(d, cb, i1 - 1, P - 1, cc, lds, L.hyp, true);
-        nmc_drain_vm();
-        if (lane == 0)
-          __hip_atomic_fetch_add(nmc_hrd(d, cb, P - 1), 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    nmc_drain_vm();
-    return;
-  }
+  // ---- register mode: the Gibbs wave runs its own loop (gibbs_step below), so its 64-value
+  //      payload never shares registers with the control code, and it meets the other
+  //      waves at the same two barriers ----
   // the register hand-off's task of step (t, p): task k = gs - lag = (kt, kq) -- poll, fetch,
   // update, and (P <= 2) this step's priors; lane 0 leaves the verdict in the flag word
   auto gibbs_step = [&](int t, int p) {
@@ -1944,7 +1845,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     if (r) {
       // keep the payload loads below the poll (no instruction: wavefront scope)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      nmc_hyper_update_reg<false>(d, cb, kt, kq, cc, lds, L.hyp, g0w);
+      nmc_hyper_update_reg(d, cb, kt, kq, cc, lds, L.hyp, g0w);
       if (p == 0) NMC_STAMP_AUX(t, 15);
       if (P <= 2) {   // the update lands in the step that needs it: this step's priors
         const int sp = gs & 1;
@@ -1959,7 +1860,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       }
     }
   };
-  if constexpr (hr && !own) if (gw) {
+  if constexpr (hr) if (gw) {
     const int gs0 = i0 * P;
     for (int t = i0; t < i1 && ok; ++t) {
       for (int p = 0; p < P; ++p) {
@@ -1984,7 +1885,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     if (ok && close_k >= 0) {
       if (nmc_wait_published(d, cb, close_k % P, (unsigned)G * (unsigned)(close_k / P - i0 + 1),
                              lds, L))
-        nmc_hyper_update_reg<false>(d, cb, close_k / P, close_k % P, cc, lds, L.hyp, true);
+        nmc_hyper_update_reg(d, cb, close_k / P, close_k % P, cc, lds, L.hyp, true);
     }
     nmc_drain_vm();
     return;
@@ -2281,9 +2182,8 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     d.ll[gc] = c_LL;
   }
   // ---- closing Gibbs updates after i1-1 (group-0 workgroups write and record them; the
-  //      owner hand-off: the last task's owner) ----
-  if constexpr (hl) if (ok && (own ? mb == 0 && nmc_task_owner(d, i1 * P - 1) == g
-                                  : hr ? close_k >= 0 : g0w)) {
+  //      register mode: the workgroups of groups 0 .. lag-1) ----
+  if constexpr (hl) if (ok && (hr ? close_k >= 0 : g0w)) {
     const int ge = i1 * P;   // tasks ge-2 (copied at the last step; P >= 2) and ge-1 are left
     if (!hr && P >= 2 && gw) {
       const size_t hvi = (((size_t)(i1 - 1 - d.vbase) * P + (P - 2)) * C + cc) * 2;
@@ -2291,7 +2191,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
                         ((ge - 2) & 1) * (G + 1));
     }
     // (register mode: the Gibbs wave closes in its own loop; this is the matching barrier)
-    const int wk = hr && !own ? close_k : ge - 1;   // the task whose publication is awaited
+    const int wk = hr ? close_k : ge - 1;   // the task whose publication is awaited
     const bool pub = nmc_wait_published(d, cb, wk % P, (unsigned)G * (unsigned)(wk / P - i0 + 1),
                                         lds, L);
     if (!hr && pub && gw) {

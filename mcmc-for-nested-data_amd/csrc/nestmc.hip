@@ -97,19 +97,12 @@ static void choose_geometry(nmc_ctx* x) {
            !(getenv("NMC_NO_HLDS") && atoi(getenv("NMC_NO_HLDS")));
   // G <= 64: the Gibbs wave fetches a task's values into registers (one sc1 round trip)
   // and updates in the step after publication (no LDS payload, no two-stage pipeline).
-  // 64 < G (at most 4 numpy leaves), opt-in NMC_HOWN=1: the owner hand-off -- task k is
-  // updated once per chain block, by the Gibbs wave of group k % G's workgroup one step
-  // after publication (the values streamed through registers in 64-value chunks, two
-  // passes), and every other workgroup reads its four results.  Bit-identical, but measured
-  // slower than the all-wave (G > 128) / LDS-payload (G <= 128) updates: 62 against 53
-  // us/iter at the cfg-4 shard, 1917 against 1654 us/iter at the cfg-5 shard -- the owner
-  // polls a task one step after its publication (a chain-block-wide wait every step) and
-  // its workgroup's barrier waits for the two streamed passes.
-  d.hown = d.naux > 0 && d.G > 64 && d.nleaf <= 4 &&
-           getenv("NMC_HOWN") && atoi(getenv("NMC_HOWN"));
-  d.hreg = d.naux > 0 && (d.G <= 64 ? d.hlds : d.hown) &&
+  // (An owner hand-off for 64 < G -- one workgroup's Gibbs wave updating each task once
+  //  for its chain block, the others reading its results -- measured slower, 62 against
+  //  53 us/iter at the cfg-4 shard, and was removed in round 5; G > 128 runs nmc_k_sweep's
+  //  Gibbs workgroups, which do the same with whole workgroups.)
+  d.hreg = d.naux > 0 && d.G <= 64 && d.hlds &&
            !(getenv("NMC_NO_HREG") && atoi(getenv("NMC_NO_HREG")));
-  if (!d.hreg) d.hown = 0;
   // Partial pooling whose grid is more than one 8-wave workgroup per CU but fits two
   // 4-wave ones (cfg-4 shards: 2 chain blocks x 256 groups): four waves, so the whole
   // grid is resident and runs persistent (both chain blocks' workgroups share each CU
@@ -129,92 +122,51 @@ static void choose_geometry(nmc_ctx* x) {
   d.paired = d.rows_lds && x->nf <= 4;
   if (const char* e = getenv("NMC_ROWS")) d.paired = d.paired && strcmp(e, "bcast") != 0;
 
-  // nmc_k_step (one barrier per step, every wave deciding) measured slower than nmc_k_run
-  // on MI355X (cfg 3: 8.8 against 8.0 us/iter, profiles/r03_step_kernel_ab.json): opt-in,
-  // NMC_STEP=1, bit-identical (tests/test_gpu_scale.py)
-  x->step_ok = getenv("NMC_STEP") && atoi(getenv("NMC_STEP")) != 0;
-  d.sflags = getenv("NMC_STEP_FLAGS") ? atoi(getenv("NMC_STEP_FLAGS")) : 0;
   // none/complete pooling whose 64-chain grid fills at most half the CUs (cfg 2: 4 chain
   // blocks x 32 groups on 256 CUs): 32 chains per workgroup, each lane pair one chain on
   // the paired loop's two row parities (NMC_MODE_HALF) -- twice the workgroups, the same
   // sums bit for bit.  NMC_HALF=0 keeps 64 chains per workgroup (tests compare them).
-  if (x->pooling != NMC_POOL_PARTIAL && d.S == 1 && d.paired && !x->step_ok &&
+  if (x->pooling != NMC_POOL_PARTIAL && d.S == 1 && d.paired &&
       (int64_t)d.RB * d.G * 2 <= x->ncu && !(getenv("NMC_HALF") && !atoi(getenv("NMC_HALF")))) {
     d.CL = 32;
     d.RB = (d.C + d.CL - 1) / d.CL;
   }
 
-  // nmc_k_sweep (sweep.h), opt-in (NMC_SWEEP=1): rows in LDS, no row split, none/complete
-  // pooling or partial pooling over one numpy leaf per Gibbs wave or the Gibbs workgroups;
-  // up to 12 waves per workgroup (three per SIMD, <= 168 VGPRs), fewer when the grid needs
-  // two or three workgroups per CU.  Bit-identical to nmc_k_run (the tests compare them);
-  // measured no faster than nmc_k_run on cfg 2 / 3 / 4 (profiles/r04m_*.json), so not
-  // the default.
+  // nmc_k_sweep (sweep.h) for partial pooling over more than one numpy leaf (G > 128, at
+  // most 4 leaves; cfg 4) with the groups' rows in LDS, no row split and a built-in family:
+  // RB * P Gibbs workgroups compute each Gibbs task once per chain block (SYNC_OWN), off the
+  // likelihood workgroups' critical path -- 31 against nmc_k_run's 52 us/iter at the cfg-4
+  // shard (profiles/r04q_cfg4_gsep.jsonl, profiles/r05).  Up to 12 waves per workgroup
+  // (three per SIMD, <= 168 VGPRs), 4 when the grid needs two or three workgroups per CU.
+  // NMC_SWEEP=0 keeps nmc_k_run.  (The sweep's other modes -- none/complete pooling and
+  // G <= 128 -- measured slower than nmc_k_run, profiles/r04m_sweep_vs_run.jsonl, and were
+  // removed in round 5.)
   x->sweep = false;
   d.gsep = 0;
-  // default: partial pooling over more than one Gibbs leaf (G > 128, cfg 4), where the
-  // Gibbs workgroups (SYNC_OWN) take the update off the critical path: 33.8 against
-  // nmc_k_run's 52.1 us/iter at the cfg-4 shard (profiles/r04q_cfg4_gsep.jsonl);
-  // NMC_SWEEP=1 everywhere it applies, NMC_SWEEP=0 never
-  const char* sw_env = getenv("NMC_SWEEP");
-  const bool sweep_want = sw_env ? atoi(sw_env) != 0
-                                 : x->pooling == NMC_POOL_PARTIAL && d.G > 128 &&
-                                       x->family < NMC_LL_USER_BASE;
-  if (d.rows_lds && d.S == 1 && !x->step_ok && !x->no_sweep && sweep_want &&
-      (x->pooling != NMC_POOL_PARTIAL || d.nleaf <= 4)) {
+  const bool sweep_want = x->pooling == NMC_POOL_PARTIAL && d.G > 128 && d.nleaf <= 4 &&
+                          x->family < NMC_LL_USER_BASE &&
+                          !(getenv("NMC_SWEEP") && !atoi(getenv("NMC_SWEEP")));
+  if (d.rows_lds && d.S == 1 && !x->no_sweep && sweep_want) {
     // (a multiple of four waves: a workgroup's waves spread evenly over the four SIMDs, so
     // two or three 4-wave workgroups per CU are resident whenever the occupancy API says so)
-    const int64_t wgs = (int64_t)d.RB * d.G +
-                        (x->pooling == NMC_POOL_PARTIAL && d.G > 128 ? (int64_t)d.RB * d.P : 0);
+    const int64_t wgs = (int64_t)d.RB * d.G + (int64_t)d.RB * d.P;
     int sw = wgs <= x->ncu ? NMC_SWEEP_THREADS / 64 : 4;
     if (const char* e = getenv("NMC_SWEEP_WAVES")) {
       const int v = atoi(e);
       if (v >= 3 && v <= NMC_SWEEP_THREADS / 64) sw = v;
     }
-    // partial pooling: a control, a Gibbs and at least one likelihood wave, all resident
-    // (G > 128, built-in families: in resident batches of chain blocks if need be, with
-    // the Gibbs workgroups as their own kernel -- nmc_create)
-    if (x->pooling != NMC_POOL_PARTIAL || wgs <= 3 * (int64_t)x->ncu ||
-        (d.G > 128 && x->family < NMC_LL_USER_BASE)) {
-      x->sweep = true;
-      d.W = sw;
-    }
-    // SYNC_OWN: the count of a publication is the start of the Gibbs workgroups' update,
-    // which every step two later waits for -- count it before the control's first tile
-    // (cfg-4 shard 30.8 vs 32.4 us/iter, profiles/r04u_ab.txt); elsewhere after it
-    d.pubearly = run_mode(x) == NMC_MODE_SYNC_OWN ? 1 : 0;
+    // a control, a Gibbs and at least one likelihood wave, all resident (in resident batches
+    // of chain blocks if need be, with the Gibbs workgroups as their own kernel: nmc_create)
+    x->sweep = true;
+    d.W = sw;
+    // the count of a publication is the start of the Gibbs workgroups' update, which every
+    // step two later waits for -- count it before the control's first tile (cfg-4 shard
+    // 30.8 vs 32.4 us/iter, profiles/r04u_ab.txt)
+    d.pubearly = 1;
     if (const char* e = getenv("NMC_PUB_EARLY")) d.pubearly = atoi(e) != 0;
-    // (SYNC_OWN's Gibbs workgroups go into their own kernel, Dev.gsep, only when the one
-    // grid cannot be resident: nmc_create; NMC_GSEP=1 forces it)
-    if (x->sweep && x->pooling == NMC_POOL_PARTIAL && d.G > 128 &&
-        x->family < NMC_LL_USER_BASE && getenv("NMC_GSEP"))
-      d.gsep = atoi(getenv("NMC_GSEP")) != 0;
-  }
-
-  // nmc_k_duo (duo.h), opt-in NMC_DUO=1: partial pooling over G <= 64 groups with the {x, y}
-  // regression rows in LDS and no row split -- two half blocks of 32 chains per workgroup
-  // stepping on their own, no step barriers.  Bit-identical to nmc_k_run (the tests compare
-  // them) but measured slower at cfg 3: 8.2-8.9 against 7.6-7.7 us/iter
-  // (profiles/r05_duo/README.md).  NMC_DUO_WAVES sets the waves (4 role waves + likelihood).
-  x->duo = false;
-  const char* duo_env = getenv("NMC_DUO");
-  if (!x->no_duo && !x->sweep && !x->step_ok && duo_env && atoi(duo_env) != 0 &&
-      x->pooling == NMC_POOL_PARTIAL && x->family == NMC_LL_LINREG && x->nf == 2 &&
-      d.G >= 2 && d.G <= 64 && d.rows_lds && d.S == 1) {
-    x->duo = true;
-    d.W = NMC_DUO_THREADS / 64;
-    if (const char* e = getenv("NMC_DUO_WAVES")) {
-      const int v = atoi(e);
-      if (v >= 3 && v <= NMC_DUO_THREADS / 64) d.W = v;
-    }
-    d.CL = 64;
-    d.RB = (d.C + 63) / 64;
-    d.paired = 0;
-    d.dkt = 2;   // likelihood tiles per ticket
-    if (const char* e = getenv("NMC_DUO_KT")) {
-      const int v = atoi(e);
-      if (v >= 1 && v <= NMC_NSLOT) d.dkt = v;
-    }
+    // (the Gibbs workgroups go into their own kernel, Dev.gsep, only when the one grid
+    // cannot be resident: nmc_create; NMC_GSEP=1 forces it)
+    if (getenv("NMC_GSEP")) d.gsep = atoi(getenv("NMC_GSEP")) != 0;
   }
 }
 
@@ -258,7 +210,7 @@ static size_t cnt_bytes(const nmc_ctx* x) {
 // The timeout word lives in coherent pinned host memory mapped into the device: the
 // kernels' (rare) system-scope store lands in host memory, so the host reads it with a
 // plain load after a synchronize -- no device-to-host copy on every synchronize.
-// owner hand-off hyper-ready counters [RB <= ceil(C / 32)][P][32]
+// nmc_k_sweep's hyper-ready counters [RB <= ceil(C / 32)][P][32]
 static size_t hrd_words(const nmc_ctx* x) { return (size_t)32 * ((x->C + 31) / 32) * x->P; }
 // Dev.gsep role words [RB <= ceil(C / 32)][16] (u64, one 128-B line per chain block)
 static size_t grole_words(const nmc_ctx* x) { return (size_t)16 * ((x->C + 31) / 32); }
@@ -485,27 +437,9 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
       choose_geometry(x);
       if (int rc2 = nmc_call_family(x, c)) { nmc_destroy(x); return rc2; }
     }
-    if (x->duo && c.result != 1) {     // the duo grid cannot be resident: nmc_k_run
-      x->no_duo = true;
-      choose_geometry(x);
-      if (int rc2 = nmc_call_family(x, c)) { nmc_destroy(x); return rc2; }
-    }
     // row split: always persistent (the members exchange every step), in resident batches
     // of chain blocks when the whole grid is not (chain blocks are independent)
     x->persistent = c.result == 1 || d.S > 1;
-  }
-  // the one-barrier step kernel runs up to 12 waves (three per SIMD) when its grid is one
-  // workgroup per CU: two likelihood waves per SIMD keep the fp64 pipe busy while the
-  // third plays a role (NMC_STEP_WAVES overrides; the tile partition, and every sum, does
-  // not depend on the wave count)
-  if (uses_step(x, run_mode(x)) && (int64_t)d.RB * d.G * d.S <= x->ncu) {
-    int w = 1 + (int)((d.nmax + 63) / 64) + (pooling == NMC_POOL_PARTIAL ? 1 : 0);
-    w = std::min(w, NMC_STEP_THREADS / 64);
-    if (const char* e = getenv("NMC_STEP_WAVES")) {
-      const int v = atoi(e);
-      if (v >= 3 && v <= NMC_STEP_THREADS / 64) w = v;
-    }
-    if (w > d.W) d.W = w;
   }
   if (d.S > 1) {   // row split: resident batches of chain blocks, exchange buffers
     NmcCall c;
@@ -529,7 +463,7 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   // build option NMC_ZIN_BUILD=1: the step kernel draws its {z, log u} itself (a job in
   // each step's tile queue) unless the opt-in one-barrier kernel runs (it DMAs them from
   // the fill's ring); NMC_ZIN=0 keeps the fill (bit-identical; tests compare them)
-  d.zin = NMC_ZIN_BUILD && !uses_step(x, run_mode(x)) &&
+  d.zin = NMC_ZIN_BUILD &&
           !(getenv("NMC_ZIN") && !atoi(getenv("NMC_ZIN")));
   // nmc_k_sweep: every variate drawn in the kernel (NMC_ZIN=1) or from the fill's ring
   if (x->sweep) d.zin = getenv("NMC_ZIN") ? (atoi(getenv("NMC_ZIN")) != 0) : 0;
@@ -936,7 +870,7 @@ int nmc_split_config(nmc_ctx* x, int* members, int* chain_blocks_per_launch) {
 int nmc_kernel_name(nmc_ctx* x, char* out, int cap) {
   static const char* const modes[] = {"NMC_MODE_NOPOOL", "NMC_MODE_LAUNCH", "NMC_MODE_SYNC",
                                       "NMC_MODE_SYNC_LDS", "NMC_MODE_SYNC_REG", "NMC_MODE_SYNC_OWN",
-                                      "NMC_MODE_HALF", "NMC_MODE_DUO"};
+                                      "NMC_MODE_HALF"};
   const int mode = run_mode(x);
   std::string fam;
   switch (x->family) {
@@ -945,19 +879,13 @@ int nmc_kernel_name(nmc_ctx* x, char* out, int cap) {
     case NMC_LL_LOGISTIC: fam = "FamLogistic<" + std::to_string(x->nf) + ">"; break;
     default: fam = "FamUser"; break;
   }
-  if (x->duo) {
-    snprintf(out, (size_t)(cap > 0 ? cap : 1), "%s", ("nmc_k_duo<" + fam + ">").c_str());
-    return cap < 1 ? fail(-1, "kernel name: cap < 1") : 0;
-  }
   if (x->sweep) {
     snprintf(out, (size_t)(cap > 0 ? cap : 1), "%s",
              ("nmc_k_sweep<" + fam + ", " + modes[mode] + ">").c_str());
     return cap < 1 ? fail(-1, "kernel name: cap < 1") : 0;
   }
-  std::string k = uses_step(x, mode)
-                      ? "nmc_k_step<" + fam + ", " + modes[mode] + ">"
-                      : "nmc_k_run<" + fam + ", " + modes[mode] + ", " +
-                            (x->d.rows_lds ? "true" : "false") + ">";
+  const std::string k = "nmc_k_run<" + fam + ", " + modes[mode] + ", " +
+                        (x->d.rows_lds ? "true" : "false") + ">";
   if (cap < 1) return fail(-1, "kernel name: cap < 1");
   snprintf(out, (size_t)cap, "%s", k.c_str());
   return 0;

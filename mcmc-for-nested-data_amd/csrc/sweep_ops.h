@@ -7,20 +7,11 @@
 #include "ctx.h"
 #include "fam_make.h"
 
-// The sweep kernel instance of a mode (for launches and occupancy queries).
+// The sweep kernel instance of a mode (for launches and occupancy queries): SYNC_OWN only
+// (partial pooling over G > 128 groups, nestmc.hip choose_geometry)
 template <class Fam>
 static const void* nmc_sweep_kernel(int mode) {
-  switch (mode) {
-    case NMC_MODE_NOPOOL: return (const void*)nmc_k_sweep<Fam, NMC_MODE_NOPOOL>;
-    case NMC_MODE_SYNC_REG: return (const void*)nmc_k_sweep<Fam, NMC_MODE_SYNC_REG>;
-    case NMC_MODE_SYNC_LDS: return (const void*)nmc_k_sweep<Fam, NMC_MODE_SYNC_LDS>;
-    case NMC_MODE_SYNC_OWN: return (const void*)nmc_k_sweep<Fam, NMC_MODE_SYNC_OWN>;
-    case NMC_MODE_HALF:   // (row pairs in every block: the host's condition)
-      if constexpr (nmc_paired_rows_ok<Fam>())
-        return (const void*)nmc_k_sweep<Fam, NMC_MODE_HALF>;
-      return nullptr;
-  }
-  return nullptr;
+  return mode == NMC_MODE_SYNC_OWN ? (const void*)nmc_k_sweep<Fam, NMC_MODE_SYNC_OWN> : nullptr;
 }
 
 // (four waves: an eight-wave form with two streams per wave needs <= 88 VGPRs to sit beside

@@ -23,28 +23,20 @@
 namespace {
 
 // kernel table entries, in name-expression order
-// (nmc_k_run: mode m (0..5) with rows in LDS at UK_RUN0 + m, rows staged at UK_RUN0 + 6 + m;
-// nmc_k_step: NOPOOL / SYNC_REG at UK_STEP0 / UK_STEP0 + 1; the half layout at UK_HALF)
-// (nmc_k_sweep: NOPOOL / SYNC_REG / SYNC_LDS / HALF / SYNC_OWN at UK_SWEEP0 + 0..4)
-enum { UK_RUN0 = 0, UK_NRUN = 6, UK_GROUP_LL = 12, UK_OBS_LL_ROWS = 13, UK_OBS_LL = 14,
-       UK_STEP0 = 15, UK_GROUP_LL_RL = 17, UK_GROUP_FIN = 18, UK_HALF = 19, UK_SWEEP0 = 20,
-       UK_N = 25 };
+// (nmc_k_run: mode m (0..4) with rows in LDS at UK_RUN0 + m, rows staged at UK_RUN0 + 5 + m;
+// the half layout at UK_HALF)
+enum { UK_RUN0 = 0, UK_NRUN = 5, UK_GROUP_LL = 10, UK_OBS_LL_ROWS = 11, UK_OBS_LL = 12,
+       UK_GROUP_LL_RL = 13, UK_GROUP_FIN = 14, UK_HALF = 15, UK_N = 16 };
 const char* const kNames[UK_N] = {
     "nmc_k_run<FamUser, 0, true>", "nmc_k_run<FamUser, 1, true>", "nmc_k_run<FamUser, 2, true>",
-    "nmc_k_run<FamUser, 3, true>", "nmc_k_run<FamUser, 4, true>", "nmc_k_run<FamUser, 5, true>",
+    "nmc_k_run<FamUser, 3, true>", "nmc_k_run<FamUser, 4, true>",
     "nmc_k_run<FamUser, 0, false>", "nmc_k_run<FamUser, 1, false>",
     "nmc_k_run<FamUser, 2, false>", "nmc_k_run<FamUser, 3, false>",
-    "nmc_k_run<FamUser, 4, false>", "nmc_k_run<FamUser, 5, false>",
+    "nmc_k_run<FamUser, 4, false>",
     "nmc_k_group_part<FamUser, false>", "nmc_k_obs_ll_rows<FamUser>",
-    "nmc_k_obs_ll<FamUser>", "nmc_k_step<FamUser, 0>", "nmc_k_step<FamUser, 4>",
-    "nmc_k_group_part<FamUser, true>", "nmc_k_group_fin<FamUser>",
-    "nmc_k_run<FamUser, 6, true>", "nmc_k_sweep<FamUser, 0>", "nmc_k_sweep<FamUser, 4>",
-    "nmc_k_sweep<FamUser, 3>", "nmc_k_sweep<FamUser, 6>", "nmc_k_sweep<FamUser, 5>"};
+    "nmc_k_obs_ll<FamUser>", "nmc_k_group_part<FamUser, true>", "nmc_k_group_fin<FamUser>",
+    "nmc_k_run<FamUser, 6, true>"};
 int run_index(const nmc_ctx* x, int mode) {
-  if (x->sweep)
-    return UK_SWEEP0 + (mode == NMC_MODE_NOPOOL ? 0 : mode == NMC_MODE_SYNC_REG ? 1
-                        : mode == NMC_MODE_SYNC_LDS ? 2 : mode == NMC_MODE_HALF ? 3 : 4);
-  if (uses_step(x, mode)) return UK_STEP0 + (mode == NMC_MODE_NOPOOL ? 0 : 1);
   if (mode == NMC_MODE_HALF) return UK_HALF;
   return UK_RUN0 + mode + (x->d.rows_lds ? 0 : UK_NRUN);
 }
@@ -84,10 +76,9 @@ int compile_kernel(UserFamily* u, int idx) {
       HIPRTC_SUCCESS)
     return nmc_fail(-2, "hiprtcCreateProgram failed");
   hiprtcAddNameExpression(prog, kNames[idx]);
-  // (the sweep kernels as the Makefile builds them: sweep_ops.h)
   const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                        u->inc.c_str(), "-mllvm", "-disable-machine-licm"};
-  const hiprtcResult r = hiprtcCompileProgram(prog, idx >= UK_SWEEP0 ? 7 : 5, opts);
+                        u->inc.c_str()};
+  const hiprtcResult r = hiprtcCompileProgram(prog, 5, opts);
   if (r != HIPRTC_SUCCESS) {
     size_t n = 0;
     hiprtcGetProgramLogSize(prog, &n);
@@ -149,21 +140,20 @@ extern "C" int nmc_user_family_compile(const char* source, int n_fields, int n_p
   u->nf = n_fields;
   u->np = n_params;
   // the library's own build-time kernel constants, so the JIT kernels index LDS and tiles
-  // exactly as the host carve (nmc_lds / nmc_step_lds / nmc_tiles) computed them
+  // exactly as the host carve (nmc_lds / nmc_tiles) computed them
   const std::string defs = "#define NMC_NSLOT_N " + std::to_string((int)NMC_NSLOT) +
                            "\n#define NMC_HYPER_NS " + std::to_string((int)NMC_HYPER_NS) +
                            "\n#define NMC_LDS_ROW_DOUBLES " +
                            std::to_string((int)NMC_LDS_ROW_DOUBLES) +
                            "\n#define NMC_RUN_THREADS " + std::to_string((int)NMC_RUN_THREADS) +
                            "\n#define NMC_ZIN_BUILD " + std::to_string((int)NMC_ZIN_BUILD) +
-                           "\n#define NMC_SWEEP_THREADS " + std::to_string((int)NMC_SWEEP_THREADS) +
                            "\n"
 #ifdef NMC_STAMPS
                            "#define NMC_STAMPS 1\n"
 #endif
       ;
   u->src = defs + "#define NMC_USER_NF " + std::to_string(n_fields) + "\n#define NMC_USER_P " +
-           std::to_string(n_params) + "\n#include \"kernels.h\"\n#include \"step.h\"\n#include \"sweep.h\"\n#line 1 \"user\"\n" + source +
+           std::to_string(n_params) + "\n#include \"kernels.h\"\n#line 1 \"user\"\n" + source +
            "\n#include \"fam_user.h\"\n";
   u->inc = std::string("-I") + include_dir;
   // the cheapest kernel now: a source error is reported here, with the compiler log
@@ -214,12 +204,9 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
         }
         Dev dd = d;
         void* args[] = {&dd, &fam, (void*)&obs, &i0, &i1, &flags};
-        struct { Dev d; FamUserArg fam; int i0, i1; } sa{d, fam, i0, i1};   // nmc_sweep_args
-        void* sargs[] = {&sa};
         hipFunction_t fr = nullptr;
         rc = user_fn(x, run_index(x, mode), &fr);
-        const dim3 gr(x->sweep && mode == NMC_MODE_SYNC_OWN ? (unsigned)sweep_grid(x) : grid.x);
-        if (!rc) rc = launch(x, fr, gr, block, lds, x->sweep ? sargs : args);
+        if (!rc) rc = launch(x, fr, grid, block, lds, args);
       });
       return rc ? rc : e;
     }
@@ -235,8 +222,7 @@ int nmc_call_user(nmc_ctx* x, NmcCall& c) {
         c.result = 0;
         return 0;
       }
-      c.result = (x->sweep ? sweep_grid(x) : (int64_t)x->d.RB * x->d.G * x->d.S) <=
-                 (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
+      c.result = (int64_t)x->d.RB * x->d.G * x->d.S <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
       return 0;
     }
     case NMC_OP_CAPACITY: {

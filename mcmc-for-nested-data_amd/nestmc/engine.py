@@ -17,7 +17,7 @@ from ._lib import as_f64, check, dptr
 # step-kernel modes reported by nmc_launch_config (kernels.h NMC_MODE_*)
 MODE_NAMES = {0: "NMC_MODE_NOPOOL", 1: "NMC_MODE_LAUNCH", 2: "NMC_MODE_SYNC",
               3: "NMC_MODE_SYNC_LDS", 4: "NMC_MODE_SYNC_REG", 5: "NMC_MODE_SYNC_OWN",
-              6: "NMC_MODE_HALF", 7: "NMC_MODE_DUO"}
+              6: "NMC_MODE_HALF"}
 
 
 class Engine:

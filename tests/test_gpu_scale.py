@@ -91,15 +91,8 @@ def test_cfg3_full_size_launch_modes_and_oracle(gpu_lib):
     # per closing workgroup, in parallel) and the publish counters carried over
     multi = _run(fam, sizes, st, sel, 0, n_iter, seed, launch_iters=5)
     assert multi[3]["mode"] == "NMC_MODE_SYNC_REG", multi[3]
-    # the opt-in twelve-wave nmc_k_sweep instead of nmc_k_run
-    fill = _run(fam, sizes, st, sel, 0, n_iter, seed, env={"NMC_SWEEP": "1"})
     assert pers[3]["kernel"].startswith("nmc_k_run<"), pers[3]
-    assert fill[3]["kernel"].startswith("nmc_k_sweep<"), fill[3]
-    # the one-barrier step kernel (opt-in) in its two proposal / Gibbs-payload variants
-    step0 = _run(fam, sizes, st, sel, 0, n_iter, seed, env={"NMC_STEP": "1"})
-    step3 = _run(fam, sizes, st, sel, 0, n_iter, seed, env={"NMC_STEP": "1", "NMC_STEP_FLAGS": "3"})
-    assert step0[3]["kernel"].startswith("nmc_k_step<"), step0[3]
-    for other in (launch, bcast, multi, fill, step0, step3):
+    for other in (launch, bcast, multi):
         for k in range(3):
             assert numpy.array_equal(pers[k], other[k], equal_nan=True), k
     acc = pers[0]
