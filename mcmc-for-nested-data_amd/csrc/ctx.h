@@ -60,6 +60,7 @@ struct nmc_ctx {
   int split_batch = 0;                    // row split: chain blocks per (resident) launch
   int sweep_batch = 0;                    // nmc_k_sweep with Dev.gsep: chain blocks per launch
   unsigned gepoch = 0;                    // Dev.gsep launches so far (Dev.gep)
+  int fill_bpc = 3;                       // nmc_k_fill blocks per CU (nmc_run)
   int gserial = 0;                        // tests (NMC_GSEP_SERIAL): the gsep kernels serialized
                                           // on one stream, 1 Gibbs kernel first, 2 second
   volatile unsigned* tmo_host = nullptr;  // host view of d.tmo (coherent pinned memory)

@@ -301,7 +301,7 @@ __device__ __forceinline__ void nmc_step_variate(const Dev& d, int it, int p, in
   } else {
     const uint32_t ch = (uint32_t)(d.chain_base + c);
     z = nmc_normal(it, g, p, NMC_PURPOSE_PROPOSAL, ch, d.seed);
-    lu = log(nmc_uniform2(it, g, p, NMC_PURPOSE_ACCEPT, ch, d.seed).a);
+    lu = nmc_log_unit(nmc_uniform2(it, g, p, NMC_PURPOSE_ACCEPT, ch, d.seed).a);
   }
 }
 
@@ -1567,6 +1567,29 @@ enum { NMC_MODE_NOPOOL = 0,      // none/complete pooling: no coupling
 // scalar-loaded (s_load, scalar cache) where a step uses them instead of being hoisted out
 // of the persistent loop and held in SGPRs for the whole launch -- some 60 fields, which
 // spilled 160-600 SGPRs per instance (MI355X: <= 102 SGPRs per wave).
+// The step loops' workgroup barrier (nmc_k_run, nmc_k_sweep): LDS traffic only.  __syncthreads() is a workgroup-scope
+// release/acquire, which waits for every outstanding global store of the wave (vmcnt(0)):
+// the control wave's write-through publish and sample stores, the Gibbs wave's hyper-state
+// stores would then sit on the step's critical path.  The step loop shares nothing through
+// global memory inside the workgroup (a wave whose LDS-DMA must have landed drains vmcnt
+// itself first), so the barrier waits for LDS operations only; the "memory" clobber keeps
+// the compiler from moving memory accesses across it.
+__device__ __forceinline__ void nmc_step_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// nmc_k_run's step barriers A and B (NMC_RUN_SYNCTHREADS=1: __syncthreads(), the A/B build)
+#ifndef NMC_RUN_SYNCTHREADS
+#define NMC_RUN_SYNCTHREADS 0
+#endif
+__device__ __forceinline__ void nmc_run_barrier() {
+#if NMC_RUN_SYNCTHREADS
+  __syncthreads();
+#else
+  nmc_step_barrier();
+#endif
+}
+
 typedef __attribute__((address_space(4))) const Dev* nmc_kdev_ptr;
 __device__ __forceinline__ const Dev* nmc_kdev() {
   nmc_kdev_ptr p = (nmc_kdev_ptr)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1675,7 +1698,17 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   double* lrows = lds + L.rows * 64;
   if constexpr (RL) {   // this group's rows -> LDS, once for the whole launch
     const int nd = nrow * Fam::NFIELDS;
-    for (int i = threadIdx.x; i < nd; i += blockDim.x) lrows[i] = grows[i];
+    if (((r0 * Fam::NFIELDS) & 1) == 0) {
+      // LDS-DMA in 16-byte pieces (global_load_lds_dwordx4: 1 KiB per wave-instruction, no
+      // VGPRs), every piece in flight at once -- one memory round trip instead of one per
+      // strided pass; an odd nd copies one double of slack (the carve has a column spare)
+      const int npc = (nd + 1) / 2;
+      for (int b0 = w * 64; b0 < npc; b0 += W * 64)
+        if (b0 + lane < npc) nmc_dma16(grows + 2 * (b0 + lane), lrows + 2 * b0);
+      nmc_drain_vm();   // (this wave's pieces have landed before the barrier below)
+    } else {
+      for (int i = threadIdx.x; i < nd; i += blockDim.x) lrows[i] = grows[i];
+    }
   }
   auto zl_src = [&](int tn, int pn) -> const double* {
     return d.vzl + ((size_t)(tn - d.vbase) * PGC + (size_t)pn * G * C + gc) * 2;
@@ -1871,12 +1904,12 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
 #if NMC_GIBBS_TILES   // (A/B build option: the Gibbs wave takes likelihood tiles after its task)
         lik_tiles(t, p, gs & 1, [] {});
 #endif
-        __syncthreads();   // A
+        nmc_run_barrier();   // A
         if (due) {
           ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
           if (!ok) break;
         }
-        __syncthreads();   // B
+        nmc_run_barrier();   // B
       }
     }
     // closing: tasks ge-lag .. ge-1, task ge-lag+j by the workgroup of group j (member 0),
@@ -2073,7 +2106,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       }
       NMC_STAMP(t, 1 + 3 * (p & 1));
       if (ctl || (hl && !pipe && gw)) nmc_drain_vm();   // this wave's LDS-DMA has landed
-      __syncthreads();
+      nmc_run_barrier();   // A
       NMC_STAMP(t, 2 + 3 * (p & 1));
 
       // ---- Gibbs update after iteration t-1 (needed by this iteration's priors) ----
@@ -2151,7 +2184,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
         if (!ok) break;
       }
       if (p == 0) NMC_STAMP(t, 3);
-      __syncthreads();      // the new value is visible to every wave
+      nmc_run_barrier();   // B: the new value is visible to every wave
     }
     NMC_STAMP(t, 6);
     if (!ok) break;

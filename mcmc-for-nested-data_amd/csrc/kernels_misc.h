@@ -5,52 +5,59 @@
 #include "kernels.h"
 
 // ---------------------------------------------------------------------------
-// Variates for iterations [iter0, iter0 + T), one launch: one thread per (t, p, c) of the
-// hyper variates {hyper z, Gamma((G-1)/2)} (Marsaglia-Tsang on the Philox stream, or
-// gammainccinv of the replayed uniform) and per (t, p, g, c) of the step variates {z,
-// log u} (nmc_step_variate).  The hyper elements come first in the index space: their
-// rejection loops are the longest threads and, started first, run under the bulk of the
-// step elements.  (Two kernels -- the step one at 92 VGPRs -- measured no faster: on one
-// stream they run back to back, and a side stream for the Gamma draws did not overlap
-// them but added a join, profiles/r03h_*.)  The ring holds at most 1 GiB, so every element
-// index fits 32 bits.
+// Variates for iterations [iter0, iter0 + T), one launch: per (t, p, c) the hyper variates
+// {hyper z, Gamma((G-1)/2)} (Marsaglia-Tsang on the Philox stream, or gammainccinv of the
+// replayed uniform) and per (t, p, g, c) the step variates {z, log u} (nmc_step_variate).
+// The hyper elements come first: their rejection loops are the longest, and started first
+// they run under the bulk of the step elements.  The ring holds at most 1 GiB, so every
+// element index fits 32 bits.
 // ---------------------------------------------------------------------------
-#ifndef NMC_FILL_MINB
-#define NMC_FILL_MINB 1
-#endif
-__global__ void __launch_bounds__(256, NMC_FILL_MINB) nmc_k_fill(Dev d, int iter0, int T) {
+// {hyper z, Gamma draw} of hyper element i = (t, p, c) of iteration it (k: its replay index)
+template <bool REPLAY>
+__device__ __forceinline__ nmc_d2 nmc_fill_hyper(const Dev& d, int it, unsigned p, unsigned c,
+                                                 size_t k) {
+  nmc_d2 h;
+  if constexpr (REPLAY) {
+    h.a = it < d.replay_n ? d.rhz[k] : nmc_nan();
+    h.b = it < d.replay_n ? nmc_igamci(d.ha, d.rhu[k], d.hlga) : nmc_nan();
+  } else {
+    const uint32_t ch = (uint32_t)(d.chain_base + (int)c);
+    h.a = nmc_normal(it, 0, p, NMC_PURPOSE_HYPER_NORMAL, ch, d.seed);
+    h.b = nmc_gamma_mt(d.ha, it, p, ch, d.seed);
+  }
+  return h;
+}
+
+// A resident grid (nmc_fill_blocks: a few 256-thread blocks per CU) walks the elements in
+// grid-stride loops, the hyper elements first: 12.9 against 18.2 us for cfg 3's 20 iterations
+// and 0.33 against 0.58 us per iteration (one thread per element: the blocks' dispatch and
+// drain dominated, profiles/r05/r05f_fillbench.json).  REPLAY: the replayed reference
+// variates (a separate instance: gammainccinv's registers would cost the Philox fill
+// occupancy).
+template <bool REPLAY>
+__global__ void __launch_bounds__(256) nmc_k_fill(Dev d, int iter0, int T) {
   const unsigned C = (unsigned)d.C, GC = (unsigned)d.G * C, PGC = (unsigned)d.P * GC;
   const unsigned PC = (unsigned)d.P * C;
   const unsigned n1 = d.zin ? 0u : (unsigned)T * PGC;   // (zin: the step kernel draws these)
   const unsigned n2 = d.pooling == NMC_POOL_PARTIAL ? (unsigned)T * PC : 0u;
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n1 + n2;
-       i += gridDim.x * blockDim.x) {
-    if (i >= n2) {   // step element i - n2
-      const unsigned e = i - n2;
-      const unsigned t = e / PGC, r = e - t * PGC;
-      const unsigned p = r / GC, q = r - p * GC;
-      const unsigned g = q / C, c = q - g * C;
-      double z, lu;
-      nmc_step_variate(d, iter0 + (int)t, (int)p, (int)g, (int)c, z, lu);
-      d.vzl[2 * (size_t)e] = z;
-      d.vzl[2 * (size_t)e + 1] = lu;
-    } else {         // hyper element i
-      const unsigned t = i / PC, r = i - t * PC;
-      const unsigned p = r / C, c = r - p * C;
-      const int it = iter0 + (int)t;
-      double hz, hx;
-      if (d.rng_mode == NMC_RNG_REPLAY) {
-        const size_t k = (size_t)it * PC + r;
-        hz = it < d.replay_n ? d.rhz[k] : nmc_nan();
-        hx = it < d.replay_n ? nmc_igamci(d.ha, d.rhu[k], d.hlga) : nmc_nan();
-      } else {
-        const uint32_t ch = (uint32_t)(d.chain_base + (int)c);
-        hz = nmc_normal(it, 0, p, NMC_PURPOSE_HYPER_NORMAL, ch, d.seed);
-        hx = nmc_gamma_mt(d.ha, it, p, ch, d.seed);
-      }
-      d.vh[2 * (size_t)i] = hz;
-      d.vh[2 * (size_t)i + 1] = hx;
-    }
+  const unsigned stride = gridDim.x * blockDim.x;
+  const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
+  for (unsigned i = tid; i < n2; i += stride) {   // hyper element i
+    const unsigned t = i / PC, r = i - t * PC;
+    const unsigned p = r / C, c = r - p * C;
+    const int it = iter0 + (int)t;
+    const nmc_d2 h = nmc_fill_hyper<REPLAY>(d, it, p, c, (size_t)it * PC + r);
+    d.vh[2 * (size_t)i] = h.a;
+    d.vh[2 * (size_t)i + 1] = h.b;
+  }
+  for (unsigned e = tid; e < n1; e += stride) {   // step element e
+    const unsigned t = e / PGC, r = e - t * PGC;
+    const unsigned p = r / GC, q = r - p * GC;
+    const unsigned g = q / C, c = q - g * C;
+    double z, lu;
+    nmc_step_variate(d, iter0 + (int)t, (int)p, (int)g, (int)c, z, lu);
+    d.vzl[2 * (size_t)e] = z;
+    d.vzl[2 * (size_t)e + 1] = lu;
   }
 }
 

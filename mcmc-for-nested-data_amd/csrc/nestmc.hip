@@ -385,6 +385,9 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   d.gpat = 200000u;
   if (const char* e = getenv("NMC_GSEP_PATIENCE_US")) d.gpat = (unsigned)(atol(e) * 100);
   x->gserial = getenv("NMC_GSEP_SERIAL") ? atoi(getenv("NMC_GSEP_SERIAL")) : 0;
+  // nmc_k_fill's grid: 3 blocks of 256 per CU (its Philox instance's 140 VGPRs: three waves
+  // per SIMD); NMC_FILL_BPC overrides (A/B)
+  x->fill_bpc = getenv("NMC_FILL_BPC") ? std::max(1, atoi(getenv("NMC_FILL_BPC"))) : 3;
   d.leaf = dleaf;
   d.merge = dmerge;
   HIPCHK(hipMemcpy(dleaf, starts.data(), starts.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -674,8 +677,15 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
                                             : (size_t)(c1 - c0) * P * x->C *
                                                   ((x->d.zin ? 0 : x->G) + (partial ? 1 : 0));
       if (n) {
-        const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);
-        hipLaunchKernelGGL(nmc_k_fill, dim3(blocks), dim3(256), 0, x->stream, x->d, c0, c1 - c0);
+        // a resident grid walking the elements (kernels_misc.h): fill_bpc blocks per CU
+        const int64_t cap = (int64_t)x->fill_bpc * x->ncu;
+        const int blocks = (int)std::min<int64_t>((int64_t)((n + 255) / 256), cap);
+        if (x->rng == NMC_RNG_REPLAY)
+          hipLaunchKernelGGL(nmc_k_fill<true>, dim3(blocks), dim3(256), 0, x->stream, x->d, c0,
+                             c1 - c0);
+        else
+          hipLaunchKernelGGL(nmc_k_fill<false>, dim3(blocks), dim3(256), 0, x->stream, x->d, c0,
+                             c1 - c0);
         HIPCHK(hipGetLastError());
       }
       // counters continue from the earlier launches (Dev.pbase / xbase): reset only

@@ -60,8 +60,82 @@ NMC_HD nmc_d2 nmc_uniform2(uint32_t it, uint32_t group, uint32_t param, uint32_t
   return nmc_d2{(double)a * inv53, (double)b * inv53};
 }
 
+// The Box-Muller transform's two transcendentals, restated for their argument ranges:
+// the library's fp64 log and cos cost 76 and 109 fp64 instructions on gfx950 (double-
+// double evaluation; cos also carries a Payne-Hanek reduction for large arguments), which
+// made every step variate 291 fp64 instructions and the fill 0.58 us per cfg-3 iteration
+// (profiles/r05/r05c_fillbench.json).  Both below are within ~1 ulp of the exact value
+// (tools/varmath_check.hip), like the library's; the oracle keeps numpy's log and cos
+// (tests compare at rtol 1e-14).
+//
+// log(x) for x in [0, 1]: x = m 2^e with m in [sqrt(1/2), sqrt(2)) (frexp, exact), log(m) =
+// 2 atanh(s), s = (m - 1) / (m + 1), |s| <= 0.1716 (m - 1 exact: Sterbenz), the series to
+// s^23 (the first omitted term < 1e-18 relative); e ln 2 in two parts (ln2_hi has 32
+// significant bits, so e * ln2_hi is exact).  0 -> -inf, NaN propagates.
+NMC_HD double nmc_log_unit(double x) {
+  int e = 0;
+  double m = frexp(x, &e);                       // m in [0.5, 1)
+  if (m < 0.70710678118654752) {
+    m = m + m;
+    e -= 1;
+  }
+  const double f = m - 1.0;
+  const double s = f / (m + 1.0);
+  const double z = s * s;
+  double q = 0.08695652173913043;                                 // 2/23
+  q = fma(q, z, 0.09523809523809523);                             // 2/21
+  q = fma(q, z, 0.10526315789473684);                             // 2/19
+  q = fma(q, z, 0.11764705882352941);                             // 2/17
+  q = fma(q, z, 0.13333333333333333);                             // 2/15
+  q = fma(q, z, 0.15384615384615385);                             // 2/13
+  q = fma(q, z, 0.18181818181818182);                             // 2/11
+  q = fma(q, z, 0.2222222222222222);                              // 2/9
+  q = fma(q, z, 0.2857142857142857);                              // 2/7
+  q = fma(q, z, 0.4);                                             // 2/5
+  q = fma(q, z, 0.6666666666666666);                              // 2/3
+  const double ed = (double)e;
+  const double l = fma(s * z, q, fma(ed, 1.9082149292705877e-10, 2.0 * s));   // + e ln2_lo
+  const double r = fma(ed, 0.6931471803691238, l);                            // + e ln2_hi
+  return x == 0.0 ? -__builtin_huge_val() : (x == x ? r : x);
+}
+
+// cos(2 pi u) for u in [0, 1) (the 53-bit uniform): reduced exactly in u -- cos(2 pi u) =
+// cos(2 pi (1 - u)) = -cos(2 pi (1/2 - v)) = sin(2 pi (1/4 - w)), every difference exact
+// (Sterbenz) -- to t in [0, 1/8] (angle <= pi/4), then the cos or sin Taylor polynomial in
+// t^2 through the t^18 / t^19 terms (the first omitted term < 1e-18 relative).
+NMC_HD double nmc_cos2pi(double u) {
+  const double v = u > 0.5 ? 1.0 - u : u;        // [0, 1/2]
+  const bool neg = v > 0.25;
+  const double w = neg ? 0.5 - v : v;            // [0, 1/4]
+  const bool sn = w > 0.125;
+  const double t = sn ? 0.25 - w : w;            // [0, 1/8]
+  const double x = t * t;
+  double c = -0.03638284114254567;
+  c = fma(c, x, 0.28200596845579123);
+  c = fma(c, x, -1.714390711088672);
+  c = fma(c, x, 7.903536371318469);
+  c = fma(c, x, -26.4262567833744);
+  c = fma(c, x, 60.24464137187666);
+  c = fma(c, x, -85.45681720669373);
+  c = fma(c, x, 64.9393940226683);
+  c = fma(c, x, -19.739208802178716);
+  c = fma(c, x, 1.0);
+  double p = -0.012031585942120627;
+  p = fma(p, x, 0.10422916220813984);
+  p = fma(p, x, -0.7181223017785006);
+  p = fma(p, x, 3.819952584848282);
+  p = fma(p, x, -15.09464257682299);
+  p = fma(p, x, 42.058693944897655);
+  p = fma(p, x, -76.70585975306139);
+  p = fma(p, x, 81.60524927607506);
+  p = fma(p, x, -41.34170224039976);
+  p = fma(p * x, t, 6.283185307179586 * t);      // sin(2 pi t)
+  const double r = sn ? p : c;
+  return neg ? -r : r;
+}
+
 NMC_HD double nmc_box_muller(double ua, double ub) {
-  return sqrt(-2.0 * log(1.0 - ua)) * cos(6.283185307179586 * ub);
+  return sqrt(-2.0 * nmc_log_unit(1.0 - ua)) * nmc_cos2pi(ub);
 }
 
 NMC_HD double nmc_normal(uint32_t it, uint32_t group, uint32_t param, uint32_t purpose,

@@ -98,17 +98,6 @@ enum { NMC_SWK_P = 0, NMC_SWK_G, NMC_SWK_C, NMC_SWK_NGRP, NMC_SWK_N, NMC_SWK_NT,
        NMC_SWK_ZL, NMC_SWK_ZM, NMC_SWK_CW, NMC_SWK_FLAG, NMC_SWK_ROWS, NMC_SWK_TOTAL,
        NMC_SWK_COUNT = 20, NMC_SWK_AT = 32 };
 
-// The step loop's workgroup barrier: LDS traffic only.  __syncthreads() is a workgroup-scope
-// release/acquire, which waits for every outstanding global store of the wave (vmcnt(0)):
-// the control wave's write-through publish and sample stores, the Gibbs wave's hyper-state
-// stores would then sit on the step's critical path.  The step loop shares nothing through
-// global memory inside the workgroup (a wave whose LDS-DMA must have landed drains vmcnt
-// itself first), so the barrier waits for LDS operations only; the "memory" clobber keeps
-// the compiler from moving memory accesses across it.
-__device__ __forceinline__ void nmc_step_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
 // Part j of the variates of step (it, p) of group g, chain c, nmc_step_variate's values
 // split three ways so three waves draw them side by side (each ~1/3 of the ~460 VALU
 // instructions): j = 0 the Box-Muller radius sqrt(-2 log(1 - ua)), j = 1 its cosine
@@ -126,9 +115,9 @@ __device__ __noinline__ double nmc_sweep_variate_part(const double* rz, const do
   }
   const nmc_d2 u = nmc_uniform2(it, g, p, j == 2 ? NMC_PURPOSE_ACCEPT : NMC_PURPOSE_PROPOSAL,
                                 ch, seed);
-  if (j == 0) return sqrt(-2.0 * log(1.0 - u.a));
-  if (j == 1) return cos(6.283185307179586 * u.b);
-  return log(u.a);
+  if (j == 0) return sqrt(-2.0 * nmc_log_unit(1.0 - u.a));
+  if (j == 1) return nmc_cos2pi(u.b);
+  return nmc_log_unit(u.a);
 }
 // {hyper z, Gamma(a) draw} of the Gibbs update of parameter q after iteration t for chain c
 // (nmc_k_fill's values: Philox normal and Marsaglia-Tsang, or the replayed reference draws

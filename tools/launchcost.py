@@ -27,9 +27,8 @@ def main():
     import bench
     ks = [int(a) for a in sys.argv[1:]] or [1, 2, 5, 10, 20, 50, 100, 400]
 
-    class A:
-        chains, groups, obs = 256, 64, 1000
-    eng, _ = bench.make_engine(A, 0, 0)
+    wl = dict(bench.WORKLOADS[os.environ.get("WORKLOAD", "cfg3")])
+    eng, _, _ = bench.make_engine(wl, 0, 1, 0)
     total = 5 + 3 * 3 * sum(ks) + 10
     eng.set_schedule(total, total // 2, 1)
     eng.set_launch_iters(0)
