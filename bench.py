@@ -322,8 +322,9 @@ def pmc_child(args):
     from nestmc import _lib
     eng, _, _ = make_engine(args.wl, 0, 1, 0)
     W, K = args.warmup, args.steps
-    eng.set_schedule(W + K, (W + K) // 2, 1)
+    eng.set_schedule(W + 2 * K, (W + 2 * K) // 2, 1)
     eng.run(0, W)
+    eng.prefill(W, W + K)
     eng.run(W, W + K)
     eng.synchronize()
     info = os.environ.get("NMC_PMC_INFO")
@@ -526,6 +527,11 @@ def main():
     # its own launch, the timed region one launch of K iterations
     eng.set_launch_iters(0)
     eng.run(0, W)
+    # the variates of the timed call, drawn as the previous call of a sampling loop draws
+    # its successor's beside its own step launch (nmc_run's pipelined fill): the timed call
+    # then draws the NEXT call's K iterations beside its step launch -- the timed region holds
+    # exactly one K-iteration fill and one K-iteration step launch (checked below)
+    eng.prefill(W, W + K)
     eng.synchronize()
 
     def barrier():
@@ -535,6 +541,7 @@ def main():
     # timed region: exactly K iterations
     barrier()
     eng.synchronize()
+    pf0 = eng.prefill_stats()
     eng.event_record(0)
     t0 = time.perf_counter()
     eng.run(W, W + K)
@@ -543,6 +550,16 @@ def main():
     eng.synchronize()
     t1 = time.perf_counter()
     barrier()
+    pf1 = eng.prefill_stats()
+    # variate fill inside the timed region: iterations drawn on the prefill stream
+    # (beside the step launches), iterations taken from the prefill made before it, and the
+    # rest drawn on the step stream ahead of their launch
+    fill = {"pipelined": pf1["issued"] > pf0["issued"] or pf1["used"] > pf0["used"],
+            "drawn_beside_step_iters": pf1["issued"] - pf0["issued"],
+            "taken_from_prefill_iters": pf1["used"] - pf0["used"],
+            "drawn_ahead_iters": K - (pf1["used"] - pf0["used"])}
+    fill["drawn_in_timed_region_iters"] = (fill["drawn_beside_step_iters"] +
+                                           fill["drawn_ahead_iters"])
     wall = t1 - t0
     ev_ms = eng.event_elapsed_ms(0, 1)
     t_rank = max(wall, ev_ms / 1e3)
@@ -660,6 +677,7 @@ def main():
             "hyper_only_avg_us": (kt["hyper_ms"] / max(1, kt["hyper_launches"])) * 1e3,
             "gather_ms": gather_ms,
             "gather_error": gather_err,
+            "variate_fill": fill,
         }
         print(json.dumps(out))
     eng.close()

@@ -119,9 +119,22 @@ int nmc_get_trace(nmc_ctx* ctx, uint8_t* accept, double* ll_prop);
 /* Sampler._loop (posteriorSampling.py:862-896) for iterations [iter_begin,
  * iter_end): StepMethod.step (:594-613) + HyperParameter.update (:463-498)
  * + the recorder (:887-889) into the device sample store.  Asynchronous on the
- * context's stream; call nmc_synchronize before reading results.            */
+ * context's stream; call nmc_synchronize before reading results.
+ * The variates of a launch chunk are drawn before it; the next chunk's (the
+ * rest of the call, then as many iterations again after it, within the
+ * schedule) are drawn on a second stream beside the chunk's step launch and
+ * taken by the chunk or call that starts there (NMC_PREFILL=0: off).  The
+ * variates depend on (seed, chain, iteration) alone: results are identical.  */
 int nmc_run(nmc_ctx* ctx, int iter_begin, int iter_end);
+/* Waits for everything nmc_run / nmc_prefill enqueued (both streams).         */
 int nmc_synchronize(nmc_ctx* ctx);
+/* Draw the variates of iterations [iter_begin, iter_end) (at most one buffer's
+ * worth) now, beside whatever runs, for a later nmc_run that starts at
+ * iter_begin: a caller that knows its next call's range (replaces nmc_run's
+ * own guess).  No effect on results.  iter_end <= the schedule's n_iter.      */
+int nmc_prefill(nmc_ctx* ctx, int iter_begin, int iter_end);
+/* Iterations drawn by prefills so far / taken by nmc_run from a prefill.      */
+int nmc_prefill_stats(nmc_ctx* ctx, int64_t* issued, int64_t* used);
 
 /* Recorded rows [row_begin, row_begin+n_rows) as [row][col][C].
  * Columns follow StepMethod.values / PartialPooling.values (:648-654, :780-787). */

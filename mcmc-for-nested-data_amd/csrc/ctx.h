@@ -32,6 +32,19 @@ struct nmc_ctx {
   hipStream_t stream = nullptr;
   hipStream_t gstream = nullptr;          // nmc_k_sweep_gibbs beside the sweep (Dev.gsep)
   hipEvent_t gev[2] = {nullptr, nullptr}; // fork / join of the two streams
+  // Pipelined variate fill (nmc_run, nmc_prefill): two variate buffers; the fill of the next
+  // chunk's (or the next call's) iterations runs on pstream into the buffer the running
+  // chunk does not read.  pf: the pending prefill -- iterations [i0, i1) into buffer buf,
+  // done at pf_ev; rd_ev[b]: the last step launch that reads buffer b.
+  hipStream_t pstream = nullptr;
+  hipEvent_t pf_ev = nullptr, rd_ev[2] = {nullptr, nullptr};
+  double* vzlb[2] = {nullptr, nullptr};
+  double* vhb[2] = {nullptr, nullptr};
+  int vbuf = 1;                           // buffer of the most recent chunk
+  struct { bool valid; int i0, i1, buf; } pf = {false, 0, 0, 0};
+  int prefill_bpc = 1;                    // prefill grid: blocks per CU (beside a step kernel)
+  bool prefill_on = true;                 // pipelined fill (NMC_PREFILL=0: off, the A/B)
+  long long pf_issued = 0, pf_used = 0;   // iterations prefilled / consumed from a prefill
   int C = 0, chain_base = 0, G = 0, P = 0, pooling = 0, family = 0, nf = 0, rng = 0;
   uint32_t seed = 0;
   int64_t n_obs = 0;

@@ -222,6 +222,60 @@ static int check_timeout(nmc_ctx* x) {
 }
 
 // ---------------------------------------------------------------------------
+// Variate fill.  nmc_run draws a chunk's variates (nmc_k_fill) before its step launch; the
+// two variate buffers let the fill of the NEXT chunk -- the rest of the call, or the same
+// length after it, the next call of a sampling loop -- run on pstream beside the step
+// launch that reads the other buffer (a prefill).  A chunk starting where the pending
+// prefill starts takes its iterations and fills only what is missing; any other chunk waits
+// for the prefill's writes and fills its own.  The variates are a function of (seed,
+// chain, iteration, ...) alone, so where they are drawn never changes a bit.
+// ---------------------------------------------------------------------------
+// iterations per step launch: launch_iters, at most a buffer's capacity
+static int fill_chunk(const nmc_ctx* x) {
+  return x->launch_iters > 0 && x->launch_iters < x->d.vcap ? x->launch_iters : x->d.vcap;
+}
+// fill elements of T iterations (nmc_k_sweep with Dev.zin draws every variate itself; the
+// step kernels with Dev.zin draw the step variates)
+static size_t fill_elements(const nmc_ctx* x, int T) {
+  if (x->sweep && x->d.zin) return 0;
+  const bool partial = x->pooling == NMC_POOL_PARTIAL;
+  return (size_t)T * x->P * x->C * ((x->d.zin ? 0 : x->G) + (partial ? 1 : 0));
+}
+// nmc_k_fill of iterations [a, b) into buffer buf, whose first iteration is vb
+static int launch_fill(nmc_ctx* x, int buf, int vb, int a, int b, hipStream_t s, int bpc) {
+  const size_t n = fill_elements(x, b - a);
+  if (!n) return 0;
+  Dev df = x->d;
+  df.vzl = x->vzlb[buf] + (size_t)(a - vb) * 2 * x->P * x->G * x->C;
+  df.vh = x->vhb[buf] + (size_t)(a - vb) * 2 * x->P * x->C;
+  df.vbase = a;
+  // a resident grid walking the elements (kernels_misc.h): bpc blocks per CU
+  const int64_t cap = (int64_t)bpc * x->ncu;
+  const int blocks = (int)std::min<int64_t>((int64_t)((n + 255) / 256), cap);
+  if (x->rng == NMC_RNG_REPLAY)
+    hipLaunchKernelGGL(nmc_k_fill<true>, dim3(blocks), dim3(256), 0, s, df, a, b - a);
+  else
+    hipLaunchKernelGGL(nmc_k_fill<false>, dim3(blocks), dim3(256), 0, s, df, a, b - a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+// prefill of iterations [a, b) (at most a buffer) into the buffer the latest chunk does not
+// read, once the last step launch reading it is done; replaces a pending prefill
+static int enqueue_prefill(nmc_ctx* x, int a, int b) {
+  b = std::min(b, a + x->d.vcap);
+  const int buf = x->vbuf ^ 1;
+  HIPCHK(hipStreamWaitEvent(x->pstream, x->rd_ev[buf], 0));
+  if (int rc = launch_fill(x, buf, a, a, b, x->pstream, x->prefill_bpc)) return rc;
+  HIPCHK(hipEventRecord(x->pf_ev, x->pstream));
+  x->pf.valid = true;
+  x->pf.i0 = a;
+  x->pf.i1 = b;
+  x->pf.buf = buf;
+  x->pf_issued += b - a;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
 extern "C" {
 
 const char* nmc_last_error(void) { return g_err.c_str(); }
@@ -288,6 +342,13 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   e = hipStreamCreateWithFlags(&x->gstream, hipStreamNonBlocking);
   if (e != hipSuccess) { nmc_destroy(x); return fail(-2, std::string("hipStreamCreate: ") + hipGetErrorString(e)); }
   for (auto& ev : x->gev) hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  e = hipStreamCreateWithFlags(&x->pstream, hipStreamNonBlocking);
+  if (e != hipSuccess) { nmc_destroy(x); return fail(-2, std::string("hipStreamCreate: ") + hipGetErrorString(e)); }
+  hipEventCreateWithFlags(&x->pf_ev, hipEventDisableTiming);
+  for (auto& ev : x->rd_ev) {   // (recorded on the empty stream: complete)
+    hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    hipEventRecord(ev, x->stream);
+  }
 
   Dev& d = x->d;
   const size_t PGC = (size_t)n_params * n_groups * n_chains, GC = (size_t)n_groups * n_chains,
@@ -388,6 +449,10 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   // nmc_k_fill's grid: 3 blocks of 256 per CU (its Philox instance's 140 VGPRs: three waves
   // per SIMD); NMC_FILL_BPC overrides (A/B)
   x->fill_bpc = getenv("NMC_FILL_BPC") ? std::max(1, atoi(getenv("NMC_FILL_BPC"))) : 3;
+  // the pipelined fill beside a step kernel: one block per CU (one wave per SIMD next to the
+  // step kernel's), NMC_PREFILL_BPC overrides; NMC_PREFILL=0 turns the pipelining off (A/B)
+  x->prefill_bpc = getenv("NMC_PREFILL_BPC") ? std::max(1, atoi(getenv("NMC_PREFILL_BPC"))) : 1;
+  x->prefill_on = !(getenv("NMC_PREFILL") && atoi(getenv("NMC_PREFILL")) == 0);
   d.leaf = dleaf;
   d.merge = dmerge;
   HIPCHK(hipMemcpy(dleaf, starts.data(), starts.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -489,12 +554,16 @@ int nmc_destroy(nmc_ctx* x) {
   if (!x) return 0;
   hipSetDevice(x->device);
   if (x->stream) hipStreamSynchronize(x->stream);
+  if (x->gstream) hipStreamSynchronize(x->gstream);
+  if (x->pstream) hipStreamSynchronize(x->pstream);
   for (void* p : x->owned) if (p) hipFree(p);
   for (auto& ev : x->ev) if (ev) hipEventDestroy(ev);
   for (auto& pr : x->kev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
   for (auto& pr : x->hev) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
-  if (x->gstream) hipStreamSynchronize(x->gstream);
   for (auto& ev : x->gev) if (ev) hipEventDestroy(ev);
+  if (x->pf_ev) hipEventDestroy(x->pf_ev);
+  for (auto& ev : x->rd_ev) if (ev) hipEventDestroy(ev);
+  if (x->pstream) hipStreamDestroy(x->pstream);
   if (x->gstream) hipStreamDestroy(x->gstream);
   if (x->stream) hipStreamDestroy(x->stream);
   if (x->tmo_host) hipHostFree((void*)x->tmo_host);
@@ -555,6 +624,9 @@ int nmc_set_replay(nmc_ctx* x, const double* z, const double* u, const double* h
   Dev& d = x->d;
   const size_t n = (size_t)n_iter * x->P * x->G * x->C, nh = (size_t)n_iter * x->P * x->C;
   double *rz, *ru, *rhz, *rhu;
+  // (a pending prefill reads the replay arrays about to be freed; its variates are stale)
+  HIPCHK(hipStreamSynchronize(x->pstream));
+  x->pf.valid = false;
   dfree(x, (void*)d.rz); dfree(x, (void*)d.ru); dfree(x, (void*)d.rhz); dfree(x, (void*)d.rhu);
   int rc = dalloc(x, &rz, n) | dalloc(x, &ru, n) | dalloc(x, &rhz, nh) | dalloc(x, &rhu, nh);
   if (rc) return rc;
@@ -592,17 +664,26 @@ int nmc_set_schedule(nmc_ctx* x, int n_iter, int burn, int thin, int tune_interv
   dfree(x, d.samples);
   int rc = dalloc(x, &d.samples, (size_t)rows * d.cols * x->C);
   if (rc) return rc;
-  // variate ring: a chunk of iterations' worth of pre-drawn variates (<= ~1 GiB)
+  // variate buffers: two chunks of iterations' worth of pre-drawn variates (<= ~1 GiB
+  // each): a chunk's step launch reads one while the next chunk's fill writes the other
   const size_t per_iter = ((size_t)2 * x->P * x->G * x->C + (size_t)2 * x->P * x->C) * 8;
   size_t budget = (size_t)1 << 30;
   if (const char* e = getenv("NMC_VARIATE_BYTES")) budget = (size_t)atoll(e);
   int vcap = (int)(budget / per_iter);
   if (vcap < 1) vcap = 1;
   if (vcap > n_iter) vcap = n_iter > 0 ? n_iter : 1;
-  dfree(x, d.vzl); dfree(x, d.vh);
+  // (a pending prefill writes the buffers about to be freed)
+  HIPCHK(hipStreamSynchronize(x->pstream));
+  x->pf.valid = false;
   const size_t PGC = (size_t)x->P * x->G * x->C, PC = (size_t)x->P * x->C;
-  rc = dalloc(x, &d.vzl, 2 * vcap * PGC) | dalloc(x, &d.vh, 2 * vcap * PC);
-  if (rc) return rc;
+  for (int b = 0; b < 2; ++b) {
+    dfree(x, x->vzlb[b]); dfree(x, x->vhb[b]);
+    rc = dalloc(x, &x->vzlb[b], 2 * vcap * PGC) | dalloc(x, &x->vhb[b], 2 * vcap * PC);
+    if (rc) return rc;
+  }
+  d.vzl = x->vzlb[0];
+  d.vh = x->vhb[0];
+  x->vbuf = 1;
   d.vcap = vcap;
   d.vbase = 0;
   x->n_iter = n_iter;
@@ -665,29 +746,40 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
     return nmc_call_family(x, c);
   };
   int rc = [&]() -> int {
-    const int chunk =
-        x->launch_iters > 0 && x->launch_iters < x->d.vcap ? x->launch_iters : x->d.vcap;
+    const int chunk = fill_chunk(x);
+    const bool fills = fill_elements(x, 1) > 0;
     for (int c0 = iter_begin; c0 < iter_end; c0 += chunk) {
       const int c1 = c0 + chunk < iter_end ? c0 + chunk : iter_end;
-      // every variate of iterations [c0, c1) in one fully parallel launch: the hyper
-      // variates (partial pooling) and the step variates (unless the step kernel draws them)
-      x->d.vbase = c0;
-      // (nmc_k_sweep with Dev.zin draws every variate itself)
-      const size_t n = x->sweep && x->d.zin ? 0
-                                            : (size_t)(c1 - c0) * P * x->C *
-                                                  ((x->d.zin ? 0 : x->G) + (partial ? 1 : 0));
-      if (n) {
-        // a resident grid walking the elements (kernels_misc.h): fill_bpc blocks per CU
-        const int64_t cap = (int64_t)x->fill_bpc * x->ncu;
-        const int blocks = (int)std::min<int64_t>((int64_t)((n + 255) / 256), cap);
-        if (x->rng == NMC_RNG_REPLAY)
-          hipLaunchKernelGGL(nmc_k_fill<true>, dim3(blocks), dim3(256), 0, x->stream, x->d, c0,
-                             c1 - c0);
-        else
-          hipLaunchKernelGGL(nmc_k_fill<false>, dim3(blocks), dim3(256), 0, x->stream, x->d, c0,
-                             c1 - c0);
-        HIPCHK(hipGetLastError());
+      // every variate of iterations [c0, c1) before the chunk's step launch: the hyper
+      // variates (partial pooling) and the step variates (unless the step kernel draws them),
+      // from the pending prefill where it starts at c0, the rest in one fully parallel launch
+      int buf = x->vbuf ^ 1, have = c0;
+      if (x->pf.valid) {
+        // (whatever it holds, the prefill's writes end before this stream goes on; no
+        // barrier packet when it is already done)
+        if (hipEventQuery(x->pf_ev) != hipSuccess)
+          HIPCHK(hipStreamWaitEvent(x->stream, x->pf_ev, 0));
+        if (x->pf.i0 == c0) {
+          buf = x->pf.buf;
+          have = std::min(c1, x->pf.i1);
+          x->pf_used += have - c0;
+        }
+        x->pf.valid = false;
       }
+      x->vbuf = buf;
+      x->d.vzl = x->vzlb[buf];
+      x->d.vh = x->vhb[buf];
+      x->d.vbase = c0;
+      if (fills && have < c1)
+        if (int rc = launch_fill(x, buf, c0, have, c1, x->stream, x->fill_bpc)) return rc;
+      // the next chunk's variates beside this chunk's step launch (enqueued after it): the
+      // rest of this call, or the same length again after it (the next call of a sampling
+      // loop) while the schedule lasts
+      int n0 = c1, n1 = c1 < iter_end ? std::min(c1 + chunk, iter_end)
+                                      : std::min({c1 + (iter_end - iter_begin), c1 + chunk,
+                                                  x->n_iter});
+      // (replayed variates: within the call only -- the replay arrays may change between calls)
+      if (!fills || !x->prefill_on || (x->rng == NMC_RNG_REPLAY && c1 == iter_end)) n1 = n0;
       // counters continue from the earlier launches (Dev.pbase / xbase): reset only
       // before they could wrap
       const uint64_t steps = (uint64_t)(c1 - c0) * P;
@@ -712,11 +804,31 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
           if (int rc = launch_run(it, it + 1, it == c0 ? NMC_RUN_HYPER_LOAD : 0)) return rc;
         if (int rc = launch_hyper(x, c1 - 1)) return rc;   // closes the chunk
       }
+      HIPCHK(hipEventRecord(x->rd_ev[buf], x->stream));
+      if (n1 > n0)
+        if (int rc = enqueue_prefill(x, n0, n1)) return rc;
     }
     return 0;
   }();
   x->cur_slot = (iter_end - 1) & 1;
   return rc;
+}
+
+int nmc_prefill(nmc_ctx* x, int iter_begin, int iter_end) {
+  hipSetDevice(x->device);
+  if (!x->scheduled) return fail(-1, "nmc_set_schedule first");
+  if (iter_begin < 0 || iter_end < iter_begin || iter_end > x->n_iter)
+    return fail(-1, "invalid iteration range");
+  if (x->rng == NMC_RNG_REPLAY && (!x->d.rz || iter_end > x->d.replay_n))
+    return fail(-1, "replay variates do not cover the iteration range");
+  if (iter_begin == iter_end || !x->prefill_on || fill_elements(x, 1) == 0) return 0;
+  return enqueue_prefill(x, iter_begin, iter_end);
+}
+
+int nmc_prefill_stats(nmc_ctx* x, int64_t* issued, int64_t* used) {
+  if (issued) *issued = x->pf_issued;
+  if (used) *used = x->pf_used;
+  return 0;
 }
 
 // Wait for the context's stream by polling it (hipStreamQuery), then blocking: the
@@ -732,16 +844,19 @@ int nmc_synchronize(nmc_ctx* x) {
     return e ? atol(e) : 50000L;
   }();
   const auto t0 = std::chrono::steady_clock::now();
-  for (;;) {
-    const hipError_t e = poll_us > 0 ? hipStreamQuery(x->stream) : hipErrorNotReady;
-    if (e == hipSuccess) break;
-    if (e != hipErrorNotReady) return fail(-2, std::string("hipStreamQuery: ") + hipGetErrorString(e));
-    const auto dt = std::chrono::steady_clock::now() - t0;
-    if (dt >= std::chrono::microseconds(poll_us)) {
-      HIPCHK(hipStreamSynchronize(x->stream));
-      break;
+  // the step stream, then the prefill stream (a prefill is part of the work a call enqueued)
+  for (hipStream_t s : {x->stream, x->pstream}) {
+    for (;;) {
+      const hipError_t e = poll_us > 0 ? hipStreamQuery(s) : hipErrorNotReady;
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) return fail(-2, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+      const auto dt = std::chrono::steady_clock::now() - t0;
+      if (dt >= std::chrono::microseconds(poll_us)) {
+        HIPCHK(hipStreamSynchronize(s));
+        break;
+      }
+      if (dt > std::chrono::microseconds(100)) std::this_thread::yield();
     }
-    if (dt > std::chrono::microseconds(100)) std::this_thread::yield();
   }
   return check_timeout(x);
 }

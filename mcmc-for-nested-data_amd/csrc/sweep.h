@@ -1029,6 +1029,7 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
       double* hy = lds + L.hyp * 64 + lane;
       double* cwv = lds + L.cw * 64 + lane;
       unsigned* tcnt = (unsigned*)(lds + L.flag * 64 + 4);   // tile queues by step parity
+      (void)G; (void)C; (void)tcnt;   // (not every instance uses them)
       const Fam& fam = A->fam;
       const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
       const int gs = t * P + p, sp = gs & 1;

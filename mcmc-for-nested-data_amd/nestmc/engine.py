@@ -127,6 +127,17 @@ class Engine:
     def synchronize(self):
         check(self.lib.nmc_synchronize(self.h))
 
+    def prefill(self, i0, i1):
+        """Draw the variates of iterations [i0, i1) now, beside whatever runs, for a later
+        run() starting at i0 (nmc_prefill; run() guesses its next call by itself)."""
+        check(self.lib.nmc_prefill(self.h, int(i0), int(i1)))
+
+    def prefill_stats(self):
+        """{"issued": iterations drawn by prefills, "used": iterations run() took from one}."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        check(self.lib.nmc_prefill_stats(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return {"issued": a.value, "used": b.value}
+
     # -- results --------------------------------------------------------------
     def samples_raw(self, row_begin=0, n_rows=None):
         """[rows][cols][C] exactly as stored on the device."""

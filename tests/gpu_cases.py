@@ -89,9 +89,10 @@ def partial_state(fam, sizes, C, P, seed=11, spread=1.0):
 
 
 def run_engine(fam, sizes, st, sel, chain_base, n_iter, seed, pooling="partial", priors=None,
-               env=None, burn=None, thin=1, tune_interval=5, launch_iters=0):
+               env=None, burn=None, thin=1, tune_interval=5, launch_iters=0, calls=None):
     """Run the HIP engine on chains ``sel`` of state ``st``; returns
-    (accept flags [C, iter, P, G], proposal LLs, recorded rows [C, rows, cols], launch config)."""
+    (accept flags [C, iter, P, G], proposal LLs, recorded rows [C, rows, cols], launch config).
+    calls: the engine calls in order, ("run" | "prefill", i0, i1) (default: one run)."""
     import os
     from nestmc.engine import Engine
     old = {}
@@ -114,11 +115,13 @@ def run_engine(fam, sizes, st, sel, chain_base, n_iter, seed, pooling="partial",
     eng.set_trace(True)
     if launch_iters:
         eng.set_launch_iters(launch_iters)
-    eng.run(0, n_iter)
+    for op, a, b in calls or [("run", 0, n_iter)]:
+        getattr(eng, op)(a, b)
     acc, llp = eng.trace(n_iter)
     rows = eng.samples()
     cfg = eng.launch_config()
     cfg["gibbs_fallbacks"] = eng.gibbs_fallbacks()
+    cfg["prefill"] = eng.prefill_stats()
     eng.close()
     return acc, llp, rows, cfg
 
