@@ -401,10 +401,13 @@ __device__ __forceinline__ int nmc_grole_own_wait(const Dev& d, int cb, int q, u
   }
 }
 // The fallback's update of task (tq, q) by one wave: HyperParameter.update (:463-498) with
-// the values streamed from global memory (sc1) in 32-value chunks -- nmc_pairwise_stream,
+// the values streamed from global memory (sc1) in 8-value chunks -- nmc_pairwise_stream,
 // the order of nmc_hyper / nmc_hyper_once -- and the task's variates from the fill's ring or
 // drawn here (Dev.zin).  write: the global slot of tq and the sample row (group 0's wave).
-__device__ __noinline__ void nmc_hyper_update_stream(const Dev& d, int cb, int tq, int q,
+// Inlined, with short chunks: a rare path (the Gibbs kernel did not run beside the sweep)
+// whose registers must not cost the likelihood loop -- as a call it added 58 SGPR spills and
+// 128 B of scratch to the cfg-4 instance; inlined with 32-value chunks, one VGPR spill.
+__device__ __forceinline__ void nmc_hyper_update_stream(const Dev& d, int cb, int tq, int q,
                                                      int cc, double* lds, int hyp, bool write) {
   const int lane = threadIdx.x & 63;
   const int P = d.P, G = d.G, C = d.C;
@@ -419,9 +422,9 @@ __device__ __noinline__ void nmc_hyper_update_stream(const Dev& d, int cb, int t
     hv.b = d.vh[hvi + 1];
   }
   const double sdm = sqrt(lds[(hyp + NMC_HY_S2 * P + q) * 64 + lane] / G);
-  const double tot = nmc_pairwise_stream<32>(d, src, false, 0.0);
+  const double tot = nmc_pairwise_stream<8>(d, src, false, 0.0);
   const double mu = tot / G + sdm * hv.a;                        // mu ~ N(mean(x), sqrt(s2/G))
-  const double ss = nmc_pairwise_stream<32>(d, src, true, mu);
+  const double ss = nmc_pairwise_stream<8>(d, src, true, mu);
   nmc_hyper_finish(d, cb, tq, q, lds, hyp, write, mu, ss, hv.b);
 }
 
