@@ -221,6 +221,22 @@ struct Dev {
 #define NMC_STAMP_AT(k, slot) do {} while (0)
 #endif
 
+// Diagnostic build only (make cstamps -> libnestmc_cst.so, never shipped): shader clock of
+// workgroup 0's waves at the step loop's phase points, steps 0..15 of a launch:
+// stamps[step * 32 + slot], slot = w (wave w arrives at barrier A), 8 (barrier A passed,
+// control), 9 (decided), 10 (barrier B passed), 16 + w (wave w's first tile starts).  Every
+// lane of the wave stores the same value (no lane-divergent store: the kernel's laundered
+// argument pointer stays scalar).
+#ifdef NMC_CSTAMPS
+#define NMC_CS(si, slot)                                                                  \
+  do {                                                                                    \
+    if (d.stamps && blockIdx.x == 0 && (si) >= 0 && (si) < 16)                            \
+      d.stamps[(si) * 32 + (slot)] = __builtin_amdgcn_s_memtime();                        \
+  } while (0)
+#else
+#define NMC_CS(si, slot) do {} while (0)
+#endif
+
 // The chain of this lane in step-kernel chain block cb (64 chains per workgroup, one per
 // lane), and whether the lane's chain exists.
 __device__ __forceinline__ int nmc_lane_chain(const Dev&, int cb, int lane) {
@@ -1823,8 +1839,15 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     // (waves 2.. start on their static entry: one LDS round trip off the step's restart)
     int kq = d.nstatic && w >= 2 ? (w - 2 < nt + zj ? w - 2 : nt + zj)
                                  : (int)__builtin_amdgcn_readlane(grab(), 0);
+#ifdef NMC_CSTAMPS
+    bool first_tile = true;
+#endif
     while (kq < nt + zj) {
       const unsigned kn = grab();
+#ifdef NMC_CSTAMPS
+      if (first_tile) NMC_CS((t - i0) * P + p, 16 + w);
+      first_tile = false;
+#endif
       if (kq < zj) {   // the variate job: {z, log u} of the next step -> the other slot
         gen_zl(tn, pn, sp ^ 1);
         kq = (int)__builtin_amdgcn_readlane(kn, 0);
@@ -1904,6 +1927,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
 #if NMC_GIBBS_TILES   // (A/B build option: the Gibbs wave takes likelihood tiles after its task)
         lik_tiles(t, p, gs & 1, [] {});
 #endif
+        NMC_CS(gs - gs0, w);
         nmc_run_barrier();   // A
         if (due) {
           ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
@@ -2106,8 +2130,10 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       }
       NMC_STAMP(t, 1 + 3 * (p & 1));
       if (ctl || (hl && !pipe && gw)) nmc_drain_vm();   // this wave's LDS-DMA has landed
+      NMC_CS(gs - gs0, w);
       nmc_run_barrier();   // A
       NMC_STAMP(t, 2 + 3 * (p & 1));
+      if (ctl) NMC_CS(gs - gs0, 8);
 
       // ---- Gibbs update after iteration t-1 (needed by this iteration's priors) ----
       // (Gibbs-wave modes: the poller's verdict is read in the same LDS batch as the
@@ -2184,7 +2210,9 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
         if (!ok) break;
       }
       if (p == 0) NMC_STAMP(t, 3);
+      if (ctl) NMC_CS(gs - gs0, 9);
       nmc_run_barrier();   // B: the new value is visible to every wave
+      if (ctl) NMC_CS(gs - gs0, 10);
     }
     NMC_STAMP(t, 6);
     if (!ok) break;

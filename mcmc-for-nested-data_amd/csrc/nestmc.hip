@@ -1335,16 +1335,16 @@ int nmc_debug_prior_logpdf(int fam, const double* prm8, const double* xs, int n,
 }
 
 // Diagnostic build only: (re)allocate and zero the stamp buffer (n > 0) and/or copy
-// it back (out != NULL): NMC_STAMP_WORDS uint64 (kernels.h, step.h for the layouts).
+// it back (out != NULL): NMC_STAMP_WORDS uint64 (kernels.h NMC_STAMP / NMC_CS layouts).
 int nmc_debug_stamps(nmc_ctx* x, int n, uint64_t* out) {
-#ifdef NMC_STAMPS
+#if defined(NMC_STAMPS) || defined(NMC_CSTAMPS)
   hipSetDevice(x->device);
   if (n > 0) {
     if (!x->d.stamps)
       if (int rc = dalloc(x, &x->d.stamps, NMC_STAMP_WORDS)) return rc;
     HIPCHK(hipMemset(x->d.stamps, 0, NMC_STAMP_WORDS * 8));
   }
-  if (out) {   // layouts: kernels.h NMC_STAMP (nmc_k_run), step.h NMC_SW / NMC_ST / NMC_SL
+  if (out) {   // layouts: kernels.h NMC_STAMP / NMC_CS (nmc_k_run), sweep.h NMC_RS_STAMP
     HIPCHK(hipStreamSynchronize(x->stream));
     HIPCHK(hipMemcpy(out, x->d.stamps, NMC_STAMP_WORDS * 8, hipMemcpyDeviceToHost));
   }
