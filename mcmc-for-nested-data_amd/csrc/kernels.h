@@ -224,7 +224,9 @@ struct Dev {
 // Diagnostic build only (make cstamps -> libnestmc_cst.so, never shipped): shader clock of
 // workgroup 0's waves at the step loop's phase points, steps 0..15 of a launch:
 // stamps[step * 32 + slot], slot = w (wave w arrives at barrier A), 8 (barrier A passed,
-// control), 9 (decided), 10 (barrier B passed), 16 + w (wave w's first tile starts).  Every
+// control), 9 (decided), 10 (barrier B passed), 16 + w (wave w's first tile starts); wave 2:
+// 11 (barrier B passed, the step before), 12 (the step's likelihood entered), 13 (proposal
+// prepared); control: 14 (slot sums done), 15 (log-likelihood finished).  Every
 // lane of the wave stores the same value (no lane-divergent store: the kernel's laundered
 // argument pointer stays scalar).
 #ifdef NMC_CSTAMPS
@@ -1805,6 +1807,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   //      takes row tiles from the step's LDS counter until none is left; `between` runs
   //      after its first tile (the control wave's pre-barrier work) ----
   auto lik_tiles = [&](int t, int p, int sp, auto&& between) {
+    if (w == 2) NMC_CS((t - i0) * P + p, 12);
     double thp[Fam::MAXP];
 #pragma unroll
     for (int q = 0; q < Fam::MAXP; ++q) thp[q] = q < P ? th[q * 64] : 0.0;
@@ -1825,6 +1828,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       }
       preg = fam.prepare(thp);
     }
+    if (w == 2) NMC_CS((t - i0) * P + p, 13);
     // the next tile is requested before the current one is computed: the atomic's
     // return rides under the tile's own row reads
     auto grab = [&]() -> unsigned {
@@ -2173,8 +2177,10 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
         if (S > 1)   // row split: every member's partials, in member order
           nmc_split_exchange(d, cb, g, mb, t * P + p - i0 * P, acc);
         if (p == 0) NMC_STAMP(t, 10);
+        NMC_CS(gs - gs0, 14);
         const double llp = fam.finish_fast(c_reg, acc, (long)ngrp, gcst);
         if (p == 0) NMC_STAMP(t, 11);
+        NMC_CS(gs - gs0, 15);
         if (hl && post_prior) {   // the Gibbs wave evaluated this step's priors
           c_lpc = cwv[NMC_CW_LPC * 64];
           c_lpp = cwv[NMC_CW_LPP * 64];
@@ -2213,6 +2219,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       if (ctl) NMC_CS(gs - gs0, 9);
       nmc_run_barrier();   // B: the new value is visible to every wave
       if (ctl) NMC_CS(gs - gs0, 10);
+      if (w == 2) NMC_CS(gs - gs0, 11);
     }
     NMC_STAMP(t, 6);
     if (!ok) break;

@@ -131,6 +131,21 @@ static void choose_geometry(nmc_ctx* x) {
     d.CL = 32;
     d.RB = (d.C + d.CL - 1) / d.CL;
   }
+  // none/complete pooling: a step's likelihood tiles go to the W - 1 waves other than the
+  // control wave (which first prepares the step).  When the 64-row tiles are a few more
+  // than those waves, one wave runs two and the step waits for it (cfg 2: 8 tiles of its
+  // 500 rows on 7 waves; the last wave reaches barrier A 2.3k cycles after the others,
+  // profiles/r05/r05s_cstamps_cfg3_cfg2.jsonl), so the tiles are sized ceil(n / (W - 1))
+  // rows instead, one per wave.  (A different tile partition: the sums' last bits.)
+  // NMC_TILE_BALANCE=0 keeps 64-row tiles (A/B).
+  if (x->pooling != NMC_POOL_PARTIAL && d.S == 1 && d.W >= 3 &&
+      !(getenv("NMC_TILE_BALANCE") && !atoi(getenv("NMC_TILE_BALANCE")))) {
+    const int64_t wt = d.W - 1, n = d.nmax, t64 = (n + 63) / 64;
+    if (t64 > wt && t64 < 2 * wt) {
+      const int64_t tile = (((n + wt - 1) / wt) + 15) & ~15;
+      if (tile <= 128) d.tile = (int)tile;
+    }
+  }
 
   // nmc_k_sweep (sweep.h) for partial pooling over more than one numpy leaf (G > 128, at
   // most 4 leaves; cfg 4) with the groups' rows in LDS, no row split and a built-in family:

@@ -55,7 +55,9 @@ def main():
         first = [rel(s[si, 16 + w]) for w in range(W)]
         rows.append({"step": si, "arrive_A": arrive, "first_tile": first,
                      "A_passed": rel(s[si, 8]), "decided": rel(s[si, 9]),
-                     "B_passed": rel(s[si, 10])})
+                     "B_passed": rel(s[si, 10]), "w2_B_prev": rel(s[si - 1, 11]),
+                     "w2_lik_entry": rel(s[si, 12]), "w2_prepared": rel(s[si, 13]),
+                     "ctl_sums": rel(s[si, 14]), "ctl_finished": rel(s[si, 15])})
     med = {}
     if rows:
         sel = [r for r in rows if r["step"] >= 2]
@@ -69,6 +71,9 @@ def main():
                "decided": float(numpy.median([r["decided"] for r in sel])),
                "B_passed": float(numpy.median([r["B_passed"] for r in sel])),
                "step_cycles": float(numpy.median([r["B_passed"] for r in sel]))}
+        for k in ("w2_B_prev", "w2_lik_entry", "w2_prepared", "ctl_sums", "ctl_finished"):
+            v = [r[k] for r in sel if r[k] is not None]
+            med[k] = float(numpy.median(v)) if v else None
     print(json.dumps({"workload": name, "K": K, "launch": lc, "median_steps_2_15": med,
                       "steps": rows}))
     eng.close()

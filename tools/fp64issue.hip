@@ -7,6 +7,7 @@
 //   dep1             : one dependent chain (latency)
 //   pb_regs          : the shipped paired linreg body (24 fp64 per 8-row block), registers only
 //   pb_lds           : the shipped paired loop with its ds_read_b128 row reads
+//   pb_lds3          : the same with three register sets, the reads two blocks ahead
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -22,17 +23,21 @@
       "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88",      \
       "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100",     \
       "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111"
+#define CL112_135                                                                              \
+  "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",      \
+      "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133",  \
+      "v134", "v135"
 
-enum { V_INDEP16 = 0, V_INDEP4, V_DEP1, V_PB_REGS, V_PB_LDS, NV };
-static const char* vname[NV] = {"indep16", "indep4", "dep1", "pb_regs", "pb_lds"};
-// fp64 wave-instructions per loop trip
-static const int vper[NV] = {48, 48, 48, 48, 48};
+enum { V_INDEP16 = 0, V_INDEP4, V_DEP1, V_PB_REGS, V_PB_LDS, V_PB_LDS3, NV };
+static const char* vname[NV] = {"indep16", "indep4", "dep1", "pb_regs", "pb_lds", "pb_lds3"};
+// fp64 wave-instructions per loop trip (pb_lds / pb_lds3: per two 8-row blocks)
+static const int vper[NV] = {48, 48, 48, 48, 48, 48};
 
 template <int V, int LB>
 __global__ void __launch_bounds__(LB) k(const double* obs, int reps, unsigned long long* ts,
                                         double* out) {
   __shared__ __attribute__((aligned(16))) double lrows[2048 + 512];
-  if (V == V_PB_LDS) {
+  if (V == V_PB_LDS || V == V_PB_LDS3) {
     for (int i = threadIdx.x; i < 2048 + 512; i += blockDim.x) lrows[i] = obs[i & 2047];
     __syncthreads();
   }
@@ -61,6 +66,37 @@ __global__ void __launch_bounds__(LB) k(const double* obs, int reps, unsigned lo
                  : [n] "+s"(n), [u0] "+v"(u0), [u1] "+v"(u1), [w0] "+v"(w0), [w1] "+v"(w1)
                  : [b0] "v"(b0), [b1] "v"(b1), [c0] "v"(c0), [c1] "v"(c1)
                  : CL64_111, "scc");
+  } else if constexpr (V == V_PB_LDS3) {
+    // three register sets, the reads of blocks i+1 and i+2 in flight while block i is
+    // consumed; 132 blocks per trip (64 two-block trips' worth of rows, counted as 66)
+    const int h = (threadIdx.x >> 5) & 1;
+    const unsigned base = (unsigned)(uintptr_t)(nmc_lds_cptr)(lrows + 2 * h);
+    for (int r = 0; r < reps; r += 66) {
+      unsigned addr = base;
+      int cnt = 132;
+      asm volatile(
+          NMC_P4(64, 0)
+          NMC_P4(88, 128)
+          "L_f_%=:\n"
+          NMC_P4(112, 256)
+          "s_waitcnt lgkmcnt(8)\n"
+          NMC_PB(64, 80)
+          NMC_P4(64, 384)
+          "s_waitcnt lgkmcnt(8)\n"
+          NMC_PB(88, 104)
+          NMC_P4(88, 512)
+          "s_waitcnt lgkmcnt(8)\n"
+          NMC_PB(112, 128)
+          "v_add_u32 %[addr], 0x180, %[addr]\n"
+          "s_sub_u32 %[cnt], %[cnt], 3\n"
+          "s_cmp_gt_i32 %[cnt], 0\n"
+          "s_cbranch_scc1 L_f_%=\n"
+          "s_waitcnt lgkmcnt(0)\n"
+          : [addr] "+v"(addr), [cnt] "+s"(cnt), [u0] "+v"(u0), [u1] "+v"(u1), [w0] "+v"(w0),
+            [w1] "+v"(w1)
+          : [b0] "v"(b0), [b1] "v"(b1), [c0] "v"(c0), [c1] "v"(c1)
+          : CL64_111, CL112_135, "scc", "memory");
+    }
   } else {
     // the shipped loop's structure (two register sets, next block's reads in flight), over
     // 128 blocks of rows per trip, the address wrapping back each trip
@@ -103,10 +139,12 @@ __global__ void __launch_bounds__(LB) k(const double* obs, int reps, unsigned lo
 
 template <int V>
 static void run(const double* obs, unsigned long long* ts, double* out) {
-  const int reps = V == V_PB_LDS ? 64 * 40 : 4000;   // pb_lds: 128 blocks (64 trips) per rep
+  // pb_lds: 128 blocks (64 trips) per rep; pb_lds3: 132 blocks (66 trips)
+  const int reps = V == V_PB_LDS ? 64 * 40 : V == V_PB_LDS3 ? 66 * 40 : 4000;
   for (int wps = 1; wps <= 4; ++wps) {
     auto kern = wps == 1 ? k<V, 256> : wps == 2 ? k<V, 512> : wps == 3 ? k<V, 768> : k<V, 1024>;
-    hipLaunchKernelGGL(kern, dim3(256), dim3(256 * wps), 0, 0, obs, V == V_PB_LDS ? 64 : 10, ts, out);
+    hipLaunchKernelGGL(kern, dim3(256), dim3(256 * wps), 0, 0, obs,
+                       V == V_PB_LDS ? 64 : V == V_PB_LDS3 ? 66 : 10, ts, out);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
@@ -156,5 +194,6 @@ int main() {
   run<V_DEP1>(obs, ts, out);
   run<V_PB_REGS>(obs, ts, out);
   run<V_PB_LDS>(obs, ts, out);
+  run<V_PB_LDS3>(obs, ts, out);
   return 0;
 }
