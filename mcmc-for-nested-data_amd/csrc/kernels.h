@@ -1639,6 +1639,10 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   const int P = d.P, G = d.G, C = d.C;
   const int b = blockIdx.x;
   const int S = d.S;
+  // the two Dev words the step's restart branches on, held for the launch (read after the
+  // per-step argument laundering they cost a scalar round trip each before the first tile)
+  const bool paired = d.paired;
+  const bool nstatic = d.nstatic;
   const int mb = b % S;                           // row-split member (S == 1: 0)
   const int g = (b / S) % G, cb = (b / S) / G + d.cb0;
   const int c = HALF ? cb * 32 + (lane & 31) : nmc_lane_chain(d, cb, lane);
@@ -1762,7 +1766,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     lds[L.flag * 64 + lane] = 0.0;
     // both tile counters start at the static entries: waves 2 .. W-1 begin on entries
     // 0 .. W-3 by rank, without a take (every wave from 2 on runs lik_tiles in every mode)
-    if (lane < 2) tcnt[lane] = (unsigned)(d.nstatic && W > 2 ? W - 2 : 0);
+    if (lane < 2) tcnt[lane] = (unsigned)(nstatic && W > 2 ? W - 2 : 0);
   }
   __syncthreads();
   NMC_RUN_SL(1);
@@ -1819,7 +1823,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     const typename Fam::Reg reg = fam.prepare(thp);
     // paired rows: the partner lane's (lane ^ 32) proposal parameters
     typename Fam::Reg preg = reg;
-    if constexpr (nmc_paired_rows_ok<Fam>() && !HALF) if (d.paired) {
+    if constexpr (nmc_paired_rows_ok<Fam>() && !HALF) if (paired) {
       const bool hi = lane >= 32;
 #pragma unroll
       for (int q = 0; q < Fam::MAXP; ++q) {
@@ -1841,8 +1845,8 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
     const int zj = NMC_ZIN_BUILD && d.zin && tn < i1 ? 1 : 0;
     // (waves 2.. start on their static entry: one LDS round trip off the step's restart)
-    int kq = d.nstatic && w >= 2 ? (w - 2 < nt + zj ? w - 2 : nt + zj)
-                                 : (int)__builtin_amdgcn_readlane(grab(), 0);
+    int kq = nstatic && w >= 2 ? (w - 2 < nt + zj ? w - 2 : nt + zj)
+                               : (int)__builtin_amdgcn_readlane(grab(), 0);
 #ifdef NMC_CSTAMPS
     bool first_tile = true;
 #endif
@@ -1864,7 +1868,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       double acc[Fam::NACC];
       if constexpr (RL) {
         bool done = false;
-        if constexpr (nmc_paired_rows_ok<Fam>()) if (HALF || d.paired) {
+        if constexpr (nmc_paired_rows_ok<Fam>()) if (HALF || paired) {
           // two chains per lane, row pairs split by lane half (half layout: one chain per
           // lane pair, each lane its row parity)
           nmc_ll_rows_lds<Fam, true, HALF>(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn,
@@ -2168,7 +2172,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       //      the Metropolis decision, one chain per lane (:334-383) ----
       if (ctl) {
         // this step's tiles are all taken; reused at step +2 (from the static entries on)
-        if (lane == 0) tcnt[sp] = (unsigned)(d.nstatic && W > 2 ? W - 2 : 0);
+        if (lane == 0) tcnt[sp] = (unsigned)(nstatic && W > 2 ? W - 2 : 0);
         double acc[Fam::NACC];
 #pragma unroll
         for (int j = 0; j < Fam::NACC; ++j) {
