@@ -322,7 +322,7 @@ def pmc_child(args):
     from nestmc import _lib
     eng, _, _ = make_engine(args.wl, 0, 1, 0)
     W, K = args.warmup, args.steps
-    eng.set_schedule(W + 2 * K, (W + 2 * K) // 2, 1)
+    eng.set_schedule(*bench_schedule(W, K))
     eng.run(0, W)
     eng.prefill(W, W + K)
     eng.run(W, W + K)
@@ -426,6 +426,22 @@ def fam_instance(kernel):
     return kernel[i + 1:].strip()
 
 
+def bench_schedule(W, K):
+    """(n_iter, burn, thin) of a run of W warm-up and 2K measured iterations: the burn-in is
+    the warm-up, so every iteration from W on -- the timed call [W, W + K) and the
+    kernel-timing call after it -- is post-burn and recorded (thin 1), the steady state of
+    the reference's sampling loop (posteriorSampling.py:883-891, every post-burn iteration
+    of the cfg written as a sample row)."""
+    return W + 2 * K, W, 1
+
+
+def recorded_in(lo, hi, n_iter, burn, thin):
+    """How many iterations of [lo, hi) write a sample row under (n_iter, burn, thin)
+    (nmc_record_row: post-burn, on the thinning grid)."""
+    first = ((burn + thin - 1) // thin) * thin
+    return sum(1 for i in range(max(lo, first), min(hi, n_iter)) if i % thin == 0)
+
+
 def _free_port():
     import socket
     with socket.socket() as s:
@@ -451,18 +467,34 @@ def spawn_ranks(args):
     port, bport = _free_port(), _free_port()
     argv = [sys.executable, os.path.abspath(__file__)] + [
         a for a in sys.argv[1:] if a not in ("--no-pmc",)] + ["--no-pmc", "--cpu-seconds", "0"]
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   NMC_BOOTSTRAP_PORT=str(bport))
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        procs.append(subprocess.Popen(argv, env=env, stdout=subprocess.PIPE, text=True))
-    outs = [p.communicate()[0] for p in procs]
-    bad = [(r, p.returncode) for r, p in enumerate(procs) if p.returncode != 0]
-    if bad:
-        print("bench.py: rank(s) failed: %s" % bad, file=sys.stderr)
-        return 1
+    import tempfile
+    procs, files = [], []
+    tmp = tempfile.mkdtemp(prefix="nmc_bench_ranks_")
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                       LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                       NMC_BOOTSTRAP_PORT=str(bport))
+            env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            # (stdout to a file, not a pipe: the ranks are polled together, none can block
+            #  on a full pipe while another is waited for)
+            files.append(open(os.path.join(tmp, "rank%d.out" % r), "w+"))
+            procs.append(subprocess.Popen(argv, env=env, stdout=files[-1], text=True,
+                                          start_new_session=True))
+        from nestmc.ranks import wait_all
+        bad = wait_all(procs)
+        if bad:
+            print("bench.py: rank(s) failed: %s" % (bad,), file=sys.stderr)
+            return 1
+        outs = []
+        for f in files:
+            f.seek(0)
+            outs.append(f.read())
+    finally:
+        for f in files:
+            f.close()
+        import shutil
+        shutil.rmtree(tmp, ignore_errors=True)
     lines = [[ln for ln in o.splitlines() if ln.startswith("{")] for o in outs]
     if not lines[0]:
         print("bench.py: rank 0 printed no JSON line", file=sys.stderr)
@@ -519,9 +551,9 @@ def main():
     device = local % n_dev
     eng, fam, C = make_engine(wl, rank, world, device)
     K, W = args.steps, args.warmup
-    n_iter = W + 2 * K
-    # schedule: record the second half like the reference (burn = n_iter // 2)
-    eng.set_schedule(n_iter, n_iter // 2, 1)
+    # schedule: the warm-up is the burn-in, every measured iteration records a sample row
+    n_iter, burn, thin = bench_schedule(W, K)
+    eng.set_schedule(n_iter, burn, thin)
     # production launch length: one persistent launch per nmc_run call (up to the
     # variate chunk), exactly as samplePosterior drives the engine -- the warmup is
     # its own launch, the timed region one launch of K iterations
@@ -572,6 +604,9 @@ def main():
     eng.run(W + K, W + 2 * K)
     kt = eng.kernel_timing()
     eng.set_kernel_timing(False)
+    # (G > 128: launches whose step kernel updated its own Gibbs tasks because the Gibbs
+    #  kernel did not run beside it -- 0 when the two kernels were co-scheduled)
+    gibbs_fb = eng.gibbs_fallbacks()
 
     gather_ms, gather_err = None, None
     if world > 1 and not args.no_gather:
@@ -639,7 +674,10 @@ def main():
             "config": {"workload": desc, "name": args.workload,
                        "chains_total": c_total, "chains_per_gpu": C, "groups": G,
                        "obs_per_group": N, "params": P, "pooling": wl["pooling"],
-                       "parallelism": "chains sharded x%d" % world, "launch": lc},
+                       "parallelism": "chains sharded x%d" % world, "launch": lc,
+                       "recorded_iters_in_timed_region": recorded_in(W, W + K, n_iter, burn,
+                                                                     thin),
+                       "gibbs_fallbacks": gibbs_fb},
             "roofline": {"bound": "valu", "achieved": valu_tips, "peak": VALU_PEAK_TIPS,
                          "unit": "T fp64 lane-instr/s",
                          "frac": None if valu_tips is None else valu_tips / VALU_PEAK_TIPS,

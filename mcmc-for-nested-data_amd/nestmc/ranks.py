@@ -23,6 +23,7 @@ import subprocess
 import sys
 import tempfile
 import time
+import types
 
 from . import _lib
 
@@ -31,6 +32,66 @@ def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def _stop(procs):
+    """Kill every child still running (each leads its own session: its whole process group)
+    and reap it."""
+    for p in procs:
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, 9)
+            except OSError:
+                pass
+            p.wait()
+
+
+def wait_all(procs, timeout=None):
+    """Wait for every rank.  Returns None when all exited 0, else the failures -- [(rank,
+    exit code)] or "timeout" -- after killing the ranks still running (they would wait on the
+    failed one in the host group's collectives).  Any exception in the caller's wait
+    (KeyboardInterrupt included) kills every rank before it propagates: no rank outlives
+    the call, none keeps writing into the output directory."""
+    deadline = None if timeout is None else time.time() + timeout
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad or (deadline is not None and time.time() > deadline):
+                _stop(procs)
+                return bad or "timeout"
+            if all(c == 0 for c in codes):
+                return None
+            time.sleep(0.02)
+    except BaseException:
+        _stop(procs)
+        raise
+
+
+class _SpecPickler(pickle.Pickler):
+    """Pickles the call for the ranks, refusing what a rank cannot unpickle: a function or
+    class defined in the caller's script (module __main__ -- e.g. a DeviceLikelihood's
+    host_function = functools.partial(computeLogLikelihood, ...) from the reference
+    examples).  A rank is a fresh interpreter running nestmc.ranks, so such names do not
+    exist there; without this check every rank would die on the unpickle and the caller see
+    only their exit codes."""
+
+    def reducer_override(self, obj):
+        if isinstance(obj, (type, types.FunctionType, types.BuiltinFunctionType)) and \
+                getattr(obj, "__module__", None) == "__main__":
+            raise ValueError(
+                "process_per_device: %r is defined in the calling script (module __main__) "
+                "and cannot be loaded by the ranks, which are separate processes; define it "
+                "in an importable module (or drop DeviceLikelihood's host_function when "
+                "startWithMLE is False: the sampler never calls it then)"
+                % getattr(obj, "__qualname__", obj))
+        return NotImplemented
+
+
+# (tests) dry-run ranks sleep this long before reporting, so a test can interrupt the parent
+# while they run
+_DRY_HOLD_S = "NMC_RANKS_DRY_HOLD_S"
+last_pids = []      # (tests) the ranks of the latest run_per_device call
 
 
 def run_per_device(kwargs, devices, dry_run=False, timeout=None):
@@ -44,39 +105,28 @@ def run_per_device(kwargs, devices, dry_run=False, timeout=None):
     try:
         spec = os.path.join(tmp, "spec.pkl")
         with open(spec, "wb") as f:
-            pickle.dump({"kwargs": kwargs, "devices": list(devices), "dir": tmp,
-                         "dry_run": bool(dry_run)}, f)
+            _SpecPickler(f).dump({"kwargs": kwargs, "devices": list(devices), "dir": tmp,
+                                  "dry_run": bool(dry_run)})
         port = _free_port()
         pkg_parent = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         pp = os.environ.get("PYTHONPATH")
         procs = []
-        for r in range(n):
-            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                       LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
-                       NMC_BOOTSTRAP_PORT=str(port),
-                       PYTHONPATH=pkg_parent + (os.pathsep + pp if pp else ""))
-            env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-            procs.append(subprocess.Popen([sys.executable, "-m", "nestmc.ranks", spec], env=env,
-                                          start_new_session=True))
-        deadline = None if timeout is None else time.time() + timeout
-        failed = None
-        while True:
-            codes = [p.poll() for p in procs]
-            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
-            if bad or (deadline is not None and time.time() > deadline):
-                failed = bad or "timeout"
-                break
-            if all(c == 0 for c in codes):
-                break
-            time.sleep(0.02)
+        del last_pids[:]
+        try:
+            for r in range(n):
+                env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                           LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                           NMC_BOOTSTRAP_PORT=str(port),
+                           PYTHONPATH=pkg_parent + (os.pathsep + pp if pp else ""))
+                env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+                procs.append(subprocess.Popen([sys.executable, "-m", "nestmc.ranks", spec],
+                                              env=env, start_new_session=True))
+                last_pids.append(procs[-1].pid)
+        except BaseException:
+            _stop(procs)
+            raise
+        failed = wait_all(procs, timeout)
         if failed is not None:
-            for p in procs:           # stop the ranks still waiting for the failed one
-                if p.poll() is None:
-                    try:
-                        os.killpg(p.pid, 9)
-                    except OSError:
-                        pass
-                    p.wait()
             raise _lib.NestmcError("samplePosterior ranks failed (rank, exit code): %s" % (failed,))
         if dry_run:
             out = []
@@ -100,6 +150,7 @@ def main(spec_path):
     kw, devices = spec["kwargs"], spec["devices"]
     if spec["dry_run"]:
         from .parallel import padded_shard
+        time.sleep(float(os.environ.get(_DRY_HOLD_S, "0") or 0))
         s0, per, real = padded_shard(kw["nChains"], world, rank)
         with open(os.path.join(spec["dir"], "dry.%d.json" % rank), "w") as f:
             json.dump({"rank": rank, "world": world, "device": devices[rank], "chain_base": s0,

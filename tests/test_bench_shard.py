@@ -108,3 +108,17 @@ def test_cpu_cores_is_the_real_budget():
     cores, aff, quota = bench.cpu_cores()
     assert aff == len(os.sched_getaffinity(0))
     assert cores == (aff if quota is None else min(aff, max(1, int(quota))))
+
+
+@pytest.mark.parametrize("W,K", [(5, 20), (200, 2000), (0, 7), (3, 1)])
+def test_timed_call_records_every_iteration(W, K):
+    """The bench schedule makes the warm-up the burn-in: every iteration of the timed call
+    [W, W + K) and of the kernel-timing call after it writes a sample row, like the post-burn
+    steady state of the reference's loop (posteriorSampling.py:883-891)."""
+    from nestmc.sampler import record_iterations
+    n_iter, burn, thin = bench.bench_schedule(W, K)
+    assert n_iter == W + 2 * K and thin == 1
+    rec = set(record_iterations(n_iter, burn, thin))
+    assert all(i in rec for i in range(W, W + 2 * K))
+    assert bench.recorded_in(W, W + K, n_iter, burn, thin) == K
+    assert bench.recorded_in(0, W, n_iter, burn, thin) == 0

@@ -58,6 +58,63 @@ def test_call_pickles_for_the_ranks():
     assert numpy.array_equal(fam(th), fam2(th))
 
 
+def test_interrupted_parent_leaves_no_rank(monkeypatch):
+    """Ctrl-C (any exception) in the parent's wait kills every rank before it propagates."""
+    import os
+    import signal
+    monkeypatch.setenv(ranks._DRY_HOLD_S, "60")      # the dry-run ranks sleep a minute
+
+    def _interrupt(signum, frame):
+        raise KeyboardInterrupt
+    old = signal.signal(signal.SIGALRM, _interrupt)
+    try:
+        signal.setitimer(signal.ITIMER_REAL, 1.5)
+        with pytest.raises(KeyboardInterrupt):
+            ranks.run_per_device(_kw(4), [0, 1], dry_run=True, timeout=120)
+    finally:
+        signal.setitimer(signal.ITIMER_REAL, 0)
+        signal.signal(signal.SIGALRM, old)
+    assert len(ranks.last_pids) == 2
+    for pid in ranks.last_pids:     # killed and reaped: no such process any more
+        with pytest.raises(ProcessLookupError):
+            os.kill(pid, 0)
+
+
+def test_main_script_callable_refused_before_spawn():
+    """A host_function defined in the caller's script cannot be unpickled by the ranks: the
+    parent refuses it with a clear error instead of N rank tracebacks."""
+    from nestmc.families import DeviceLikelihood
+
+    def computeLogLikelihood(parameter):
+        return numpy.zeros(parameter.shape[1])
+    computeLogLikelihood.__module__ = "__main__"     # as if defined in the user's script
+    kw = _kw(4)
+    kw["logLikelihoodFunction"] = DeviceLikelihood(
+        numpy.zeros((40, 2)), "__device__ double nmc_user_loglik(const double* t, "
+        "const double* r, const double* k) { return 0.0; }", 2,
+        host_function=computeLogLikelihood)
+    del ranks.last_pids[:]
+    with pytest.raises(ValueError, match="__main__"):
+        ranks.run_per_device(kw, [0, 1], dry_run=True, timeout=120)
+    assert ranks.last_pids == []     # nothing was started
+
+
+def test_bench_spawn_waits_for_every_rank():
+    """bench.py's rank spawn polls every rank and stops the rest on the first failure
+    (nestmc.ranks.wait_all)."""
+    import subprocess
+    import sys
+    import time
+    ok = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"],
+                          start_new_session=True)
+    bad = subprocess.Popen([sys.executable, "-c", "import sys; sys.exit(3)"],
+                           start_new_session=True)
+    t0 = time.time()
+    assert ranks.wait_all([ok, bad], timeout=100) == [(1, 3)]
+    assert time.time() - t0 < 30
+    assert ok.returncode is not None      # killed and reaped
+
+
 def test_process_per_device_refuses_chain_subsets():
     from nestmc.sampler import sample_posterior
     kw = _kw(4)
