@@ -44,6 +44,7 @@ struct FamUser {
     return n == 0 ? 0.0 : acc[0];
   }
   __device__ __forceinline__ double gconst(long) const { return 0.0; }
+  __device__ __forceinline__ void hold() {}   // (families.h FamLinreg::hold; no constants)
   __device__ __forceinline__ double finish_fast(const Reg& r, const double* acc, long n,
                                                 double) const {
     return finish(r, acc, n);

@@ -93,6 +93,10 @@ struct FamLinreg {
   __device__ __forceinline__ double gconst(long n) const {
     return sigma_known > 0.0 ? (double)n * (NMC_LOG_C + log_sigma_known) : 0.0;
   }
+  // finish_fast's constants held in registers for a persistent launch (a local copy of the
+  // family): the step kernels read the kernel arguments through a pointer laundered every
+  // step, so 1 / sigma^2 would otherwise be a scalar load on the decision's critical path
+  __device__ __forceinline__ void hold() { asm volatile("" : "+v"(inv_s2_known)); }
   // finish() on the decision's critical path: known sigma -> one multiply-add.
   __device__ __forceinline__ double finish_fast(const Reg& r, const double* acc, long n,
                                                 double gc) const {
@@ -171,6 +175,10 @@ struct FamGaussMean {
     for (int j = 0; j < NF; ++j) c += (double)n * (NMC_LOG_C + lsd[j]);
     return c;
   }
+  __device__ __forceinline__ void hold() {   // (FamLinreg::hold)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) asm volatile("" : "+v"(isd2[j]));
+  }
   __device__ __forceinline__ double finish_fast(const Reg&, const double* acc, long n,
                                                 double gc) const {
     if (n == 0) return 0.0;
@@ -235,6 +243,7 @@ struct FamLogistic {
     return n == 0 ? 0.0 : acc[0];
   }
   __device__ __forceinline__ double gconst(long) const { return 0.0; }
+  __device__ __forceinline__ void hold() {}   // (FamLinreg::hold; no constants)
   __device__ __forceinline__ double finish_fast(const Reg& r, const double* acc, long n,
                                                 double) const {
     return finish(r, acc, n);

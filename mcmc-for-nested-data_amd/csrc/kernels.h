@@ -52,6 +52,8 @@ struct Dev {
   // cfg 3 and was removed.)
   int CL, RB;
   int paired;            // likelihood rows: two chains per lane (nmc_ll_rows_lds<Fam, true>)
+  int quad;              // nmc_k_run, {x, y} rows in LDS: four chains per lane
+                         // (nmc_ll_rows_lds_quad; NMC_ROWS=pair keeps the paired loop)
   // Row split (none/complete pooling with large groups): S workgroups ("members") share
   // one (chain block, group), member m owning the m-th contiguous chunk of the group's
   // rows (nmc_chunk); each step they exchange their partial sums through xbuf
@@ -267,6 +269,11 @@ enum { NMC_RUN_HYPER_LOAD = 1 };
 #endif
 #ifndef NMC_GIBBS_TILES
 #define NMC_GIBBS_TILES 0
+#endif
+// nmc_k_run: the control wave takes its likelihood tiles at priority 0 (1), or keeps its
+// priority 3 throughout (0)
+#ifndef NMC_CTL_TILE_PRIO
+#define NMC_CTL_TILE_PRIO 1
 #endif
 #ifndef NMC_TILE_TAPER
 #define NMC_TILE_TAPER 0
@@ -851,6 +858,120 @@ __device__ __forceinline__ void nmc_rows_lds_linreg2_paired(const double* p, int
         "v164", "v165", "v166", "v167", "scc", "memory");
 }
 
+// The quad-chain form (Dev.quad, the default for {x, y} rows): a wave's four quarters (rows
+// of 16 lanes) read rows 4m+q of every 16-row block, q = the lane's quarter, and every lane
+// evaluates its row for FOUR chains -- those of lanes (lane & 15) + 16j, j = 0..3, the same
+// position in each quarter -- so one ds_read_b128 feeds 256 (chain, row) terms: a quarter
+// of the broadcast loop's LDS reads and half the paired loop's, and 48 fp64 instructions
+// per four reads, which keeps one wave's issue off the LDS latency.  Chain slot j's
+// accumulator a[j] in quarter q sums rows = q (mod 4) in row order: exactly the broadcast
+// loop's a[q] of chain (lane & 15) + 16j (its 8-row blocks put row i into a[i & 3]), so a
+// 4 x 4 transpose across the quarters (nmc_transpose4) hands every lane its own chain's
+// a[0..3] and the sums are bit-identical to the broadcast and paired loops.
+// Registers: row sets v[120:135] / v[136:151] (block b+1's four reads in flight while block
+// b is consumed), residual temporaries v[152:167] -- the paired loop's range, so the kernel's
+// register budget is unchanged.  p: this quarter's first row (tile start + q rows);
+// nb: 16-row blocks >= 1, any count.
+#define NMC_Q4(b, off)                                                     \
+  "ds_read_b128 v[" #b "+0:" #b "+3], %[addr] offset:" #off "+0\n"         \
+  "ds_read_b128 v[" #b "+4:" #b "+7], %[addr] offset:" #off "+64\n"        \
+  "ds_read_b128 v[" #b "+8:" #b "+11], %[addr] offset:" #off "+128\n"      \
+  "ds_read_b128 v[" #b "+12:" #b "+15], %[addr] offset:" #off "+192\n"
+// chain slot j of a row (x at v[xr], y at v[yr]) into temporary t: t = c_j - y, then
+// t = fma(x, d_j, t), then a_j = fma(t, t, a_j) -- FamLinreg::accum's operations
+#define NMC_QD(t, yr, j) "v_add_f64 v[" #t ":" #t "+1], %[c" #j "], -v[" #yr ":" #yr "+1]\n"
+#define NMC_QE(t, xr, j) \
+  "v_fma_f64 v[" #t ":" #t "+1], v[" #xr ":" #xr "+1], %[d" #j "], v[" #t ":" #t "+1]\n"
+#define NMC_QS(t, j) "v_fma_f64 %[a" #j "], v[" #t ":" #t "+1], v[" #t ":" #t "+1], %[a" #j "]\n"
+// two rows (x0/y0, then x1/y1) for the four chain slots: 8 adds, 8 fmas, 8 accumulations
+// (slot j gets row x0 before row x1, the row order)
+#define NMC_QH(x0, y0, x1, y1)                                                               \
+  NMC_QD(152, y0, 0) NMC_QD(154, y0, 1) NMC_QD(156, y0, 2) NMC_QD(158, y0, 3)                \
+  NMC_QD(160, y1, 0) NMC_QD(162, y1, 1) NMC_QD(164, y1, 2) NMC_QD(166, y1, 3)                \
+  NMC_QE(152, x0, 0) NMC_QE(154, x0, 1) NMC_QE(156, x0, 2) NMC_QE(158, x0, 3)                \
+  NMC_QE(160, x1, 0) NMC_QE(162, x1, 1) NMC_QE(164, x1, 2) NMC_QE(166, x1, 3)                \
+  NMC_QS(152, 0) NMC_QS(154, 1) NMC_QS(156, 2) NMC_QS(158, 3)                                \
+  NMC_QS(160, 0) NMC_QS(162, 1) NMC_QS(164, 2) NMC_QS(166, 3)
+// a 16-row block from register set A (v[120:135]) / B (v[136:151]): its rows 4m+q, m = 0..3
+#define NMC_QBA NMC_QH(120, 122, 124, 126) NMC_QH(128, 130, 132, 134)
+#define NMC_QBB NMC_QH(136, 138, 140, 142) NMC_QH(144, 146, 148, 150)
+__device__ __forceinline__ void nmc_rows_lds_linreg2_quad(const double* p, int nb,
+                                                          const double (&c)[4],
+                                                          const double (&dd)[4],
+                                                          double (&a)[4]) {
+  unsigned addr = (unsigned)(uintptr_t)(nmc_lds_cptr)p;
+  int cnt = nb;
+  asm volatile(
+      NMC_Q4(120, 0)
+      "L_nmc_q_%=:\n"
+      "s_sub_u32 %[cnt], %[cnt], 1\n"
+      "s_cmp_gt_i32 %[cnt], 0\n"
+      "s_cbranch_scc0 L_nmc_qla_%=\n"
+      NMC_Q4(136, 256)
+      "s_waitcnt lgkmcnt(4)\n"
+      NMC_QBA
+      "v_add_u32 %[addr], 0x200, %[addr]\n"
+      "s_sub_u32 %[cnt], %[cnt], 1\n"
+      "s_cmp_gt_i32 %[cnt], 0\n"
+      "s_cbranch_scc0 L_nmc_qlb_%=\n"
+      NMC_Q4(120, 0)
+      "s_waitcnt lgkmcnt(4)\n"
+      NMC_QBB
+      "s_branch L_nmc_q_%=\n"
+      "L_nmc_qla_%=:\n"
+      "s_waitcnt lgkmcnt(0)\n"
+      NMC_QBA
+      "s_branch L_nmc_qend_%=\n"
+      "L_nmc_qlb_%=:\n"
+      "s_waitcnt lgkmcnt(0)\n"
+      NMC_QBB
+      "L_nmc_qend_%=:\n"
+      : [addr] "+v"(addr), [cnt] "+s"(cnt), [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]),
+        [a3] "+v"(a[3])
+      : [c0] "v"(c[0]), [c1] "v"(c[1]), [c2] "v"(c[2]), [c3] "v"(c[3]), [d0] "v"(dd[0]),
+        [d1] "v"(dd[1]), [d2] "v"(dd[2]), [d3] "v"(dd[3])
+      : "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130",
+        "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141",
+        "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152",
+        "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161", "v162", "v163",
+        "v164", "v165", "v166", "v167", "scc", "memory");
+}
+
+// v of the four lanes (lane & 15) + 16j, j = 0..3 (the lane's position in each quarter):
+// v_permlane16_swap exchanges odd rows of its first operand with even rows of its second
+// (rows of 16 lanes), v_permlane32_swap the upper half of the first with the lower half of
+// the second (gfx950); swapping a value with itself yields its row pair / half pair
+__device__ __forceinline__ void nmc_quarters(double v, double (&o)[4]) {
+  const unsigned l = (unsigned)__double2loint(v), h = (unsigned)__double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(l, l, false, false);   // [0]: row 2k, [1]: 2k+1
+  const auto b = __builtin_amdgcn_permlane16_swap(h, h, false, false);
+  const nmc_pair2 ev = nmc_halves(__hiloint2double((int)b[0], (int)a[0]));   // rows 0, 2
+  const nmc_pair2 od = nmc_halves(__hiloint2double((int)b[1], (int)a[1]));   // rows 1, 3
+  o[0] = ev.lo;
+  o[1] = od.lo;
+  o[2] = ev.hi;
+  o[3] = od.hi;
+}
+template <bool R16>
+__device__ __forceinline__ void nmc_swap_rows(double& x, double& y) {
+  const unsigned xl = (unsigned)__double2loint(x), xh = (unsigned)__double2hiint(x);
+  const unsigned yl = (unsigned)__double2loint(y), yh = (unsigned)__double2hiint(y);
+  const auto l = R16 ? __builtin_amdgcn_permlane16_swap(xl, yl, false, false)
+                     : __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
+  const auto h = R16 ? __builtin_amdgcn_permlane16_swap(xh, yh, false, false)
+                     : __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
+  x = __hiloint2double((int)h[0], (int)l[0]);
+  y = __hiloint2double((int)h[1], (int)l[1]);
+}
+// a[j] of quarter q -> a[q] of quarter j (4 x 4 transpose over the quarters): half swaps of
+// (a0, a2), (a1, a3), then row swaps of (a0, a1), (a2, a3)
+__device__ __forceinline__ void nmc_transpose4(double (&a)[4]) {
+  nmc_swap_rows<false>(a[0], a[2]);
+  nmc_swap_rows<false>(a[1], a[3]);
+  nmc_swap_rows<true>(a[0], a[1]);
+  nmc_swap_rows<true>(a[2], a[3]);
+}
+
 // The same over rows staged in LDS: blocks of R rows read with wave-uniform
 // (broadcast) ds_reads; block b+1 is requested before block b is consumed (LDS
 // returns in order, so the wait covers only block b).
@@ -993,6 +1114,42 @@ __device__ __forceinline__ void nmc_ll_rows_lds(const Fam& fam, const typename F
   for (int k = 0; k < Fam::NACC; ++k) acc[k] = (a[0][k] + a[1][k]) + (a[2][k] + a[3][k]);
 }
 
+// The quad-chain row loop (nmc_rows_lds_linreg2_quad) over one tile of n rows at p: c / dd
+// hold the intercept and slope of the four chains of the lane's quarter position
+// (nmc_quarters).  The 16-row blocks cover the broadcast loop's even number of 8-row blocks;
+// after the transpose the lane's own chain's four accumulators take the remaining rows in
+// order into a[0], as in nmc_ll_rows_lds -- every sum bit-identical to it.
+template <class Fam>
+__device__ __forceinline__ void nmc_ll_rows_lds_quad(const Fam& fam, const typename Fam::Reg& reg,
+                                                     const double* __restrict__ p, int n,
+                                                     double (&acc)[Fam::NACC],
+                                                     const double (&c)[4], const double (&dd)[4]) {
+  static_assert(Fam::ASM_ROWS && Fam::NFIELDS == 2 && Fam::NACC == 1, "{x, y} rows only");
+  constexpr int NF = Fam::NFIELDS;
+  const int q = (threadIdx.x >> 4) & 3;
+  const int nb16 = (n / 8) >> 1;      // = the broadcast loop's (n / 8) & ~1 8-row blocks / 2
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  if (nb16 > 0) {
+    nmc_rows_lds_linreg2_quad(p + (size_t)q * NF, nb16, c, dd, a);
+    nmc_transpose4(a);
+  }
+  double at[1] = {a[0]};
+  constexpr int TB = 8;
+  for (int r0 = nb16 * 16; r0 < n; r0 += TB) {
+    double tv[TB * NF];
+#pragma unroll
+    for (int i = 0; i < TB; ++i) {
+      const int rr = r0 + i < n ? r0 + i : n - 1;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) tv[i * NF + f] = p[(size_t)rr * NF + f];
+    }
+#pragma unroll
+    for (int i = 0; i < TB; ++i)
+      if (r0 + i < n) fam.accum(reg, tv + i * NF, at);
+  }
+  acc[0] = (at[0] + a[1]) + (a[2] + a[3]);
+}
+
 // ---------------------------------------------------------------------------
 // Rows that do not fit LDS (groups over 64 KiB): each wave stages its tile through two
 // private LDS buffers of NMC_SR(NF) rows, copied by LDS-DMA (global_load_lds_dwordx4, no
@@ -1077,10 +1234,40 @@ __device__ __forceinline__ void nmc_ll_rows_staged(const Fam& fam, const typenam
 // The tile partials of one sum in a fixed order: tile k into accumulator k % 4, combined
 // (a0+a1)+(a2+a3); every LDS read in flight at once (slots past the last tile hold -0.0,
 // and x + (-0.0) == x).
+typedef double nmc_v2d __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ double nmc_sum_slots(const double* pt) {
   double v[NMC_NSLOT];
+#if NMC_NSLOT_N == 16
+  // the 16 slots (512 B apart) as eight ds_read2st64_b64, all in flight, one wait: left to
+  // itself the scheduler splits them over two LDS round trips on the decision's path
+  {
+    const unsigned a = (unsigned)(uintptr_t)(nmc_lds_cptr)pt;
+    nmc_v2d r[8];
+    asm volatile(
+        "ds_read2st64_b64 %0, %8 offset1:1\n\t"
+        "ds_read2st64_b64 %1, %8 offset0:2 offset1:3\n\t"
+        "ds_read2st64_b64 %2, %8 offset0:4 offset1:5\n\t"
+        "ds_read2st64_b64 %3, %8 offset0:6 offset1:7\n\t"
+        "ds_read2st64_b64 %4, %8 offset0:8 offset1:9\n\t"
+        "ds_read2st64_b64 %5, %8 offset0:10 offset1:11\n\t"
+        "ds_read2st64_b64 %6, %8 offset0:12 offset1:13\n\t"
+        "ds_read2st64_b64 %7, %8 offset0:14 offset1:15\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]),
+          "=&v"(r[6]),
+          "=&v"(r[7])
+        : "v"(a)
+        : "memory");
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      v[2 * u] = r[u].x;
+      v[2 * u + 1] = r[u].y;
+    }
+  }
+#else
 #pragma unroll
   for (int u = 0; u < NMC_NSLOT; ++u) v[u] = pt[u * 64];
+#endif
   double a4[4];
 #pragma unroll
   for (int u = 0; u < NMC_NSLOT; ++u) a4[u & 3] = u < 4 ? v[u] : a4[u & 3] + v[u];
@@ -1642,6 +1829,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   // the two Dev words the step's restart branches on, held for the launch (read after the
   // per-step argument laundering they cost a scalar round trip each before the first tile)
   const bool paired = d.paired;
+  const bool quad = d.quad;
   const bool nstatic = d.nstatic;
   const int mb = b % S;                           // row-split member (S == 1: 0)
   const int g = (b / S) % G, cb = (b / S) / G + d.cb0;
@@ -1717,6 +1905,15 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     }
   }
   const double gcst = fam.gconst((long)ngrp);   // per-group constant of finish_fast
+  // the decision's family constants (finish_fast) and publish targets (this lane's value of
+  // parameter 0 in vb0 / vb1), held in registers for the launch: read through the per-step
+  // laundered argument pointer they are scalar round trips on the decision's critical path,
+  // and barrier B's lgkmcnt(0) waits for them
+  Fam fh = fam;
+  fh.hold();
+  double* pub0 = d.vb0 + gc;
+  double* pub1 = d.vb1 + gc;
+  asm volatile("" : "+v"(pub0), "+v"(pub1));
   double* lrows = lds + L.rows * 64;
   if constexpr (RL) {   // this group's rows -> LDS, once for the whole launch
     const int nd = nrow * Fam::NFIELDS;
@@ -1786,6 +1983,12 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   double q_plp = 0, q_pll = 0;
   // the rest of a decided step's state update (:369-383, :608-610): counters, log prior,
   // log-likelihood, sample and trace rows
+  // its sample / trace stores wait in registers (w_*) until store_pending, which the control
+  // wave issues after the step's publication count: the count's vmcnt drain then waits for
+  // the publish store alone, not for stores issued just before it
+  int w_q = -1, w_t = 0;
+  bool w_acc = false;
+  double w_v = 0, w_ll = 0;
   auto apply_pending = [&]() {
     const int q = pend_p, tq = pend_t;
     st[(NMC_ST_LP * P + q) * 64] = q_plp;
@@ -1793,19 +1996,29 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     st[(NMC_ST_NR * P + q) * 64] = cwv[(q_acc ? NMC_CW_NRA : NMC_CW_NRR) * 64];
     st[(NMC_ST_TA * P + q) * 64] = cwv[NMC_CW_TA * 64] + (q_acc ? 1.0 : 0.0);
     if (q_acc) c_LL = q_pll;
+    w_q = q;
+    w_t = tq;
+    w_v = th[q * 64];
+    w_acc = q_acc;
+    w_ll = q_pll;
+    pend_p = -1;
+  };
+  auto store_pending = [&]() {
+    if (w_q < 0) return;
+    const int q = w_q, tq = w_t;
     if (live) {
       const int row = nmc_record_row(d, tq);
       if (row >= 0) {
         const int col = q * (G + (PARTIAL ? 2 : 0)) + (PARTIAL ? 2 : 0) + g;
-        d.samples[((size_t)row * d.cols + col) * C + c] = th[q * 64];
+        d.samples[((size_t)row * d.cols + col) * C + c] = w_v;
       }
       if (tq < d.trace_n) {
         const size_t it = (((size_t)tq * P + q) * G + g) * C + c;
-        d.tflag[it] = q_acc ? 1 : 0;
-        d.tllp[it] = q_pll;
+        d.tflag[it] = w_acc ? 1 : 0;
+        d.tllp[it] = w_ll;
       }
     }
-    pend_p = -1;
+    w_q = -1;
   };
   // ---- the likelihood of step (t, p)'s proposal (:615-635), tile by tile: the wave
   //      takes row tiles from the step's LDS counter until none is left; `between` runs
@@ -1813,17 +2026,27 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   auto lik_tiles = [&](int t, int p, int sp, auto&& between) {
     if (w == 2) NMC_CS((t - i0) * P + p, 12);
     double thp[Fam::MAXP];
+    double vp = 0.0;   // thp[p] (a select per parameter: no dynamically indexed array)
 #pragma unroll
-    for (int q = 0; q < Fam::MAXP; ++q) thp[q] = q < P ? th[q * 64] : 0.0;
-    const double prop = thp[p] + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
-                                     lds[(L.zl + 2 * sp) * 64 + 2 * lane];
+    for (int q = 0; q < Fam::MAXP; ++q) {
+      thp[q] = q < P ? th[q * 64] : 0.0;
+      if (q == p) vp = thp[q];
+    }
+    const double prop = vp + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
+                                 lds[(L.zl + 2 * sp) * 64 + 2 * lane];
 #pragma unroll
     for (int q = 0; q < Fam::MAXP; ++q)
       if (q == p) thp[q] = prop;
     const typename Fam::Reg reg = fam.prepare(thp);
+    // quad rows: intercept and slope of the four chains of this lane's quarter position
+    double qc[4], qd[4];
+    if constexpr (Fam::ASM_ROWS && RL && !HALF) if (quad) {
+      nmc_quarters(reg.b0, qc);
+      nmc_quarters(reg.b[0], qd);
+    }
     // paired rows: the partner lane's (lane ^ 32) proposal parameters
     typename Fam::Reg preg = reg;
-    if constexpr (nmc_paired_rows_ok<Fam>() && !HALF) if (paired) {
+    if constexpr (nmc_paired_rows_ok<Fam>() && !HALF) if (paired && !quad) {
       const bool hi = lane >= 32;
 #pragma unroll
       for (int q = 0; q < Fam::MAXP; ++q) {
@@ -1868,7 +2091,11 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       double acc[Fam::NACC];
       if constexpr (RL) {
         bool done = false;
-        if constexpr (nmc_paired_rows_ok<Fam>()) if (HALF || paired) {
+        if constexpr (Fam::ASM_ROWS && !HALF) if (quad) {
+          nmc_ll_rows_lds_quad(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc, qc, qd);
+          done = true;
+        }
+        if constexpr (nmc_paired_rows_ok<Fam>()) if (!done && (HALF || paired)) {
           // two chains per lane, row pairs split by lane half (half layout: one chain per
           // lane pair, each lane its row parity)
           nmc_ll_rows_lds<Fam, true, HALF>(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn,
@@ -1901,7 +2128,9 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     const int gs = t * P + p;
     if (gs - lag < i0 * P) return;
     const int k = gs - lag, kq = k % P, kt = k / P;
+    NMC_CS(gs - i0 * P, 24);
     const bool r = nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1));
+    NMC_CS(gs - i0 * P, 25);
     if (lane == 0)
       __hip_atomic_store(lds + L.flag * 64 + 1, r ? 2.0 * ((double)gs + 1) : -2.0 * ((double)gs + 1),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1909,7 +2138,17 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     if (r) {
       // keep the payload loads below the poll (no instruction: wavefront scope)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef NMC_CSTAMPS
+      {   // (diagnostics: the fetch and the update stamped apart)
+        double xv[64], fz, fx;
+        nmc_hyper_fetch_reg(d, kt, kq, cc, xv, fz, fx);
+        NMC_CS(gs - i0 * P, 26);
+        nmc_hyper_compute_reg(d, cb, kt, kq, lds, L.hyp, g0w, fz, fx, xv);
+        NMC_CS(gs - i0 * P, 27);
+      }
+#else
       nmc_hyper_update_reg(d, cb, kt, kq, cc, lds, L.hyp, g0w);
+#endif
       if (p == 0) NMC_STAMP_AUX(t, 15);
       if (P <= 2) {   // the update lands in the step that needs it: this step's priors
         const int sp = gs & 1;
@@ -1922,6 +2161,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
             t > 0 ? nmc_norm_logpdf_r(v, m, sd, isd, lsd) : st[(NMC_ST_LP * P + p) * 64];
         cwv[NMC_CW_LPP * 64] = nmc_norm_logpdf_r(prop, m, sd, isd, lsd);
       }
+      NMC_CS(gs - i0 * P, 28);
     }
   };
   if constexpr (hr) if (gw) {
@@ -1958,7 +2198,6 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
 
   for (int t = i0; t < i1 && ok; ++t) {
     NMC_STAMP(t, 0);
-    const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
     for (int p = 0; p < P; ++p) {
       dP = nmc_kdev();
       const int sp = (t * P + p) & 1;
@@ -2083,6 +2322,9 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
           double naA = na + 1.0, nrA = nr, naR = na, nrR = nr + 1.0;
           c_sA = s;
           c_sR = s;
+          // (tuning is the control wave's alone: evaluated here, the burn-in and interval
+          //  loads and the division stay off the other waves' restart)
+          const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
           if (tune) {
             nmc_tune(c_sA, naA, nrA);
             nmc_tune(c_sR, naR, nrR);
@@ -2106,8 +2348,16 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
             c_lpp = nmc_prior_logpdf(d.pfam[p], d.ppar + 8 * p, c_prop);
           }
         }
-        if constexpr (hr) {   // count the previous step's value published: its store has had
-                              // the pre-work above to drain (the Gibbs waves poll two steps on)
+      };
+      // ---- the control wave's memory work, last before its tiles: the count of the previous
+      //      step's publication (register Gibbs mode: after the pre-work above, so the publish
+      //      store has drained), then the pending sample / trace stores (issued after the count,
+      //      whose vmcnt wait then covers the publish store alone) and the next step's variate
+      //      DMA.  (Deferring this work until after the control wave's first tile measured
+      //      slower: 15.4-15.6 against 14.7-15.0 ms per 2 000 iterations, profiles/r06.)
+      auto ctl_post = [&]() {
+        if constexpr (hr) {   // count the previous step's value published (the Gibbs waves
+                              // poll it two steps on)
           if (pub_p >= 0) {
             nmc_drain_vm();
             if (lane == 0)
@@ -2116,26 +2366,21 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
             pub_p = -1;
           }
         }
+        store_pending();
         const int tn = p + 1 < P ? t : t + 1;
         const int pn = p + 1 < P ? p + 1 : 0;
         if (tn < i1 && !(NMC_ZIN_BUILD && d.zin)) put_zl(tn, pn, sp ^ 1);   // (zin: the job)
-            };
-      bool ctl_done = !ctl;
+      };
       if (ctl) {
         ctl_work();
-        ctl_done = true;
+        ctl_post();
       }
+      // the control wave's tiles at the issue priority of the tile waves (its SIMD partner is
+      // one of them); the decision after barrier A runs at priority 3 again
+      if (ctl && NMC_CTL_TILE_PRIO && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(0);
       // ---- likelihood of the proposal (:615-635), tile by tile, every wave ----
-      lik_tiles(t, p, sp, [&]() {
-        if (!ctl_done) {
-          ctl_work();
-          ctl_done = true;
-        }
-      });
-      if (!ctl_done) {   // (no tile left for the control wave)
-        ctl_work();
-        ctl_done = true;
-      }
+      lik_tiles(t, p, sp, [] {});
+      if (ctl && NMC_CTL_TILE_PRIO && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
       NMC_STAMP(t, 1 + 3 * (p & 1));
       if (ctl || (hl && !pipe && gw)) nmc_drain_vm();   // this wave's LDS-DMA has landed
       NMC_CS(gs - gs0, w);
@@ -2182,7 +2427,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
           nmc_split_exchange(d, cb, g, mb, t * P + p - i0 * P, acc);
         if (p == 0) NMC_STAMP(t, 10);
         NMC_CS(gs - gs0, 14);
-        const double llp = fam.finish_fast(c_reg, acc, (long)ngrp, gcst);
+        const double llp = fh.finish_fast(c_reg, acc, (long)ngrp, gcst);
         if (p == 0) NMC_STAMP(t, 11);
         NMC_CS(gs - gs0, 15);
         if (hl && post_prior) {   // the Gibbs wave evaluated this step's priors
@@ -2202,7 +2447,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
         th[p * 64] = vn;
         if constexpr (sync) {   // publish write-through; counted at the next step's start
           if (live)
-            __hip_atomic_store(((t & 1) ? d.vb1 : d.vb0) + (size_t)p * G * C + gc, vn,
+            __hip_atomic_store(((t & 1) ? pub1 : pub0) + (size_t)p * G * C, vn,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (mb == 0) pub_p = p;   // (row split: member 0 publishes and counts)
         }
@@ -2239,6 +2484,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   }
 
   if (ctl && pend_p >= 0) apply_pending();
+  if (ctl) store_pending();
   // ---- epilogue: state back to HBM (control wave) ----
   if (ctl && live && ok) {
     double* vo = ((i1 - 1) & 1) ? d.vb1 : d.vb0;

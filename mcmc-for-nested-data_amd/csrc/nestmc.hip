@@ -63,6 +63,9 @@ static void choose_geometry(nmc_ctx* x) {
   if (w > 8) w = 8;   // (a 768-thread build runs 12 only when asked: NMC_WAVES)
   if (w < 1) w = 1;
   d.CL = 64;   // one chain per lane, every kernel
+  // the wave count from the rows alone: the none/complete-pooling tile balance below sizes
+  // the tiles from it, so the NMC_WAVES override never changes a sum
+  const int64_t w_rows = w;
   if (const char* e = getenv("NMC_WAVES")) {
     const int v = atoi(e);
     if (v >= 1 && v <= NMC_RUN_THREADS / 64) w = v;
@@ -121,6 +124,11 @@ static void choose_geometry(nmc_ctx* x) {
   // reads; NMC_ROWS=bcast keeps the one-chain broadcast loop (same sums bit for bit)
   d.paired = d.rows_lds && x->nf <= 4;
   if (const char* e = getenv("NMC_ROWS")) d.paired = d.paired && strcmp(e, "bcast") != 0;
+  // {x, y} rows (linear regression with one covariate): four chains per lane instead
+  // (kernels.h nmc_ll_rows_lds_quad, nmc_k_run only), the same sums bit for bit;
+  // NMC_ROWS=pair keeps the paired loop
+  d.quad = d.paired && x->family == NMC_LL_LINREG && x->nf == 2;
+  if (const char* e = getenv("NMC_ROWS")) d.quad = d.quad && strcmp(e, "pair") != 0;
 
   // none/complete pooling whose 64-chain grid fills at most half the CUs (cfg 2: 4 chain
   // blocks x 32 groups on 256 CUs): 32 chains per workgroup, each lane pair one chain on
@@ -136,11 +144,16 @@ static void choose_geometry(nmc_ctx* x) {
   // than those waves, one wave runs two and the step waits for it (cfg 2: 8 tiles of its
   // 500 rows on 7 waves; the last wave reaches barrier A 2.3k cycles after the others,
   // profiles/r05/r05s_cstamps_cfg3_cfg2.jsonl), so the tiles are sized ceil(n / (W - 1))
-  // rows instead, one per wave.  (A different tile partition: the sums' last bits.)
-  // NMC_TILE_BALANCE=0 keeps 64-row tiles (A/B).
-  if (x->pooling != NMC_POOL_PARTIAL && d.S == 1 && d.W >= 3 &&
-      !(getenv("NMC_TILE_BALANCE") && !atoi(getenv("NMC_TILE_BALANCE")))) {
-    const int64_t wt = d.W - 1, n = d.nmax, t64 = (n + 63) / 64;
+  // rows instead, one per wave.  (A different tile partition: the sums' last bits.)  The
+  // partition depends on the rows only (w_rows, not the launched W, which NMC_WAVES may
+  // override), so every sum stays independent of the wave count.  The A/B knob
+  // NMC_TILE_BALANCE=0 (64-row tiles) changes sums and exists in diagnostic builds only.
+  bool balance = true;
+#ifdef NMC_DEBUG_KNOBS
+  if (getenv("NMC_TILE_BALANCE") && !atoi(getenv("NMC_TILE_BALANCE"))) balance = false;
+#endif
+  if (x->pooling != NMC_POOL_PARTIAL && d.S == 1 && w_rows >= 3 && balance) {
+    const int64_t wt = w_rows - 1, n = d.nmax, t64 = (n + 63) / 64;
     if (t64 > wt && t64 < 2 * wt) {
       const int64_t tile = (((n + wt - 1) / wt) + 15) & ~15;
       if (tile <= 128) d.tile = (int)tile;

@@ -280,8 +280,13 @@ def test_cfg2_full_size_half_layout(gpu_lib):
                       priors=priors, env={"NMC_HALF": "0"})
     assert half[3]["mode"] == "NMC_MODE_HALF" and half[3]["chains_per_block"] == 32, half[3]
     assert full[3]["mode"] == "NMC_MODE_NOPOOL", full[3]
+    # the balanced tiles (500 rows: 80-row tiles for the 7 likelihood waves) come from the
+    # rows alone -- a launch with a different wave count sums the same tiles
+    w4 = run_engine(fam, sizes, st, numpy.arange(C), 0, n_iter, seed, pooling=pooling,
+                    priors=priors, env={"NMC_WAVES": "4"})
     for k in range(3):
         assert numpy.array_equal(half[k], full[k], equal_nan=True), k
+        assert numpy.array_equal(half[k], w4[k], equal_nan=True), k
     assert 0.05 < half[0].mean() < 0.95
     sel = numpy.array([0, 1, 255])
     _check_vs_oracle(half, nested, st, sel, sel, n_iter, seed, pooling=pooling, priors=priors)

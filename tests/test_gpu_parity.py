@@ -193,15 +193,18 @@ def test_eval_group_ll_matches_oracle(gpu_lib):
 ])
 def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
     """The paired-chain row loop (each lane evaluates its row pair half for its own chain
-    and for lane ^ 32's, kernels.h nmc_ll_rows_lds<Fam, true>) reproduces the one-chain
-    broadcast loop bit for bit: flags, proposal LLs and recorded rows; so does the 64-chain
-    layout where none pooling runs the half layout."""
+    and for lane ^ 32's, kernels.h nmc_ll_rows_lds<Fam, true>) and, for {x, y} rows, the
+    quad-chain loop (each lane evaluates rows 4m+q for the four chains of its quarter
+    position, nmc_ll_rows_lds_quad; the default) reproduce the one-chain broadcast loop bit
+    for bit: flags, proposal LLs and recorded rows; so does the 64-chain layout where none
+    pooling runs the half layout."""
     from gpu_cases import run_engine
     fam, sizes, priors, pooling, names = synthetic(kind, C, G, N, ragged=ragged)
     P = fam.n_params
     st, _ = _synthetic_state(fam, sizes, priors, pooling, C, P, len(sizes))
     runs = {}
     envs = {"paired": {"NMC_ROWS": "paired"}, "bcast": {"NMC_ROWS": "bcast"},
+            "pair": {"NMC_ROWS": "pair"},     # the paired loop where the quad loop is default
             # none pooling on few workgroups runs the half layout (32 chains per workgroup,
             # lane pairs on the two row parities); this keeps 64 chains per workgroup
             "full": {"NMC_HALF": "0"}}
@@ -216,4 +219,5 @@ def test_paired_rows_bit_identical(gpu_lib, kind, C, G, N, ragged, n_iter):
     for k in range(3):
         assert numpy.array_equal(runs["paired"][k], runs["bcast"][k], equal_nan=True), k
         assert numpy.array_equal(runs["paired"][k], runs["full"][k], equal_nan=True), k
+        assert numpy.array_equal(runs["paired"][k], runs["pair"][k], equal_nan=True), k
     assert runs["paired"][0].mean() > 0.02

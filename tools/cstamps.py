@@ -57,7 +57,12 @@ def main():
                      "A_passed": rel(s[si, 8]), "decided": rel(s[si, 9]),
                      "B_passed": rel(s[si, 10]), "w2_B_prev": rel(s[si - 1, 11]),
                      "w2_lik_entry": rel(s[si, 12]), "w2_prepared": rel(s[si, 13]),
-                     "ctl_sums": rel(s[si, 14]), "ctl_finished": rel(s[si, 15])})
+                     "ctl_sums": rel(s[si, 14]), "ctl_finished": rel(s[si, 15]),
+                     # the register-mode Gibbs wave (wave 1): entered its task, poll
+                     # succeeded, payload fetched, update done, priors done
+                     "g_enter": rel(s[si, 24]), "g_polled": rel(s[si, 25]),
+                     "g_fetched": rel(s[si, 26]), "g_updated": rel(s[si, 27]),
+                     "g_priors": rel(s[si, 28])})
     med = {}
     if rows:
         sel = [r for r in rows if r["step"] >= 2]
@@ -71,7 +76,8 @@ def main():
                "decided": float(numpy.median([r["decided"] for r in sel])),
                "B_passed": float(numpy.median([r["B_passed"] for r in sel])),
                "step_cycles": float(numpy.median([r["B_passed"] for r in sel]))}
-        for k in ("w2_B_prev", "w2_lik_entry", "w2_prepared", "ctl_sums", "ctl_finished"):
+        for k in ("w2_B_prev", "w2_lik_entry", "w2_prepared", "ctl_sums", "ctl_finished",
+                  "g_enter", "g_polled", "g_fetched", "g_updated", "g_priors"):
             v = [r[k] for r in sel if r[k] is not None]
             med[k] = float(numpy.median(v)) if v else None
     print(json.dumps({"workload": name, "K": K, "launch": lc, "median_steps_2_15": med,
