@@ -93,10 +93,13 @@ struct FamLinreg {
   __device__ __forceinline__ double gconst(long n) const {
     return sigma_known > 0.0 ? (double)n * (NMC_LOG_C + log_sigma_known) : 0.0;
   }
-  // finish_fast's constants held in registers for a persistent launch (a local copy of the
-  // family): the step kernels read the kernel arguments through a pointer laundered every
-  // step, so 1 / sigma^2 would otherwise be a scalar load on the decision's critical path
-  __device__ __forceinline__ void hold() { asm volatile("" : "+v"(inv_s2_known)); }
+  // the family's constants held in registers for a persistent launch (a local copy of the
+  // family): the step kernel's loop is built without machine loop-invariant code motion, so
+  // 1 / sigma^2 (finish_fast) and the layout words prepare() branches on would otherwise be
+  // scalar loads of the kernel argument on the decision's and the restart's critical paths
+  __device__ __forceinline__ void hold() {
+    asm volatile("" : "+v"(inv_s2_known), "+v"(sigma_known), "+v"(intercept));
+  }
   // finish() on the decision's critical path: known sigma -> one multiply-add.
   __device__ __forceinline__ double finish_fast(const Reg& r, const double* acc, long n,
                                                 double gc) const {

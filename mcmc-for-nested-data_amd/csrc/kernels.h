@@ -417,6 +417,13 @@ __device__ __forceinline__ void nmc_dma16(const double* src_lane, double* lds_ds
   __builtin_amdgcn_global_load_lds((nmc_glb_ptr)src_lane, (nmc_lds_ptr)lds_dst, 16, 0, 0);
 }
 __device__ __forceinline__ void nmc_drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Write-through store of v to global memory -- what __hip_atomic_store(relaxed, agent scope)
+// emits for a global pointer (global_store_dwordx2 ... sc1) -- for an address held in VGPRs
+// whose address space the compiler no longer sees: it would emit a flat store, which counts
+// in lgkmcnt as well, and the LDS-only step barrier would then wait for its write-through.
+__device__ __forceinline__ void nmc_store_wt(double* p, double v) {
+  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
 
 // ---------------------------------------------------------------------------
 // Gibbs update of the hyper-parameters after iteration t for chain block cb
@@ -1831,6 +1838,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   const bool paired = d.paired;
   const bool quad = d.quad;
   const bool nstatic = d.nstatic;
+  const bool ctlprio = NMC_CTL_TILE_PRIO && !(d.noprio & 1);
   const int mb = b % S;                           // row-split member (S == 1: 0)
   const int g = (b / S) % G, cb = (b / S) / G + d.cb0;
   const int c = HALF ? cb * 32 + (lane & 31) : nmc_lane_chain(d, cb, lane);
@@ -1909,7 +1917,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   // parameter 0 in vb0 / vb1), held in registers for the launch: read through the per-step
   // laundered argument pointer they are scalar round trips on the decision's critical path,
   // and barrier B's lgkmcnt(0) waits for them
-  Fam fh = fam;
+  Fam fh = fam;   // (used for every family call below)
   fh.hold();
   double* pub0 = d.vb0 + gc;
   double* pub1 = d.vb1 + gc;
@@ -2025,19 +2033,22 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   //      after its first tile (the control wave's pre-barrier work) ----
   auto lik_tiles = [&](int t, int p, int sp, auto&& between) {
     if (w == 2) NMC_CS((t - i0) * P + p, 12);
+    // every LDS read of the restart issued before any is used: one round trip (left alone
+    // the scheduler waits for the values before it issues the scale and variate reads)
+    const double sv = st[(NMC_ST_S * P + p) * 64], zv = lds[(L.zl + 2 * sp) * 64 + 2 * lane];
     double thp[Fam::MAXP];
+#pragma unroll
+    for (int q = 0; q < Fam::MAXP; ++q) thp[q] = q < P ? th[q * 64] : 0.0;
+    __builtin_amdgcn_sched_barrier(0);
     double vp = 0.0;   // thp[p] (a select per parameter: no dynamically indexed array)
 #pragma unroll
-    for (int q = 0; q < Fam::MAXP; ++q) {
-      thp[q] = q < P ? th[q * 64] : 0.0;
+    for (int q = 0; q < Fam::MAXP; ++q)
       if (q == p) vp = thp[q];
-    }
-    const double prop = vp + (1.0 * st[(NMC_ST_S * P + p) * 64]) *
-                                 lds[(L.zl + 2 * sp) * 64 + 2 * lane];
+    const double prop = vp + (1.0 * sv) * zv;
 #pragma unroll
     for (int q = 0; q < Fam::MAXP; ++q)
       if (q == p) thp[q] = prop;
-    const typename Fam::Reg reg = fam.prepare(thp);
+    const typename Fam::Reg reg = fh.prepare(thp);
     // quad rows: intercept and slope of the four chains of this lane's quarter position
     double qc[4], qd[4];
     if constexpr (Fam::ASM_ROWS && RL && !HALF) if (quad) {
@@ -2053,7 +2064,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
         const nmc_pair2 e = nmc_halves(thp[q]);
         thp[q] = hi ? e.lo : e.hi;
       }
-      preg = fam.prepare(thp);
+      preg = fh.prepare(thp);
     }
     if (w == 2) NMC_CS((t - i0) * P + p, 13);
     // the next tile is requested before the current one is computed: the atomic's
@@ -2092,24 +2103,24 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       if constexpr (RL) {
         bool done = false;
         if constexpr (Fam::ASM_ROWS && !HALF) if (quad) {
-          nmc_ll_rows_lds_quad(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc, qc, qd);
+          nmc_ll_rows_lds_quad(fh, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc, qc, qd);
           done = true;
         }
         if constexpr (nmc_paired_rows_ok<Fam>()) if (!done && (HALF || paired)) {
           // two chains per lane, row pairs split by lane half (half layout: one chain per
           // lane pair, each lane its row parity)
-          nmc_ll_rows_lds<Fam, true, HALF>(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn,
+          nmc_ll_rows_lds<Fam, true, HALF>(fh, reg, lrows + (size_t)ra * Fam::NFIELDS, rn,
                                            acc, &preg);
           done = true;
         }
         if (!done)   // wave-uniform LDS address: broadcast ds_reads, pipelined
-          nmc_ll_rows_lds(fam, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
+          nmc_ll_rows_lds(fh, reg, lrows + (size_t)ra * Fam::NFIELDS, rn, acc);
       } else if constexpr (Fam::NFIELDS <= 4) {
         // rows beyond LDS, narrow rows: blocks of >= 4 rows per scalar load run ahead in
         // the scalar cache (the staged loop measured 1.7x slower for 2-field rows)
-        nmc_ll_rows(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, acc);
+        nmc_ll_rows(fh, reg, grows + (size_t)ra * Fam::NFIELDS, rn, acc);
       } else {          // wide rows beyond LDS: staged per wave by LDS-DMA, two chunks deep
-        nmc_ll_rows_staged(fam, reg, grows + (size_t)ra * Fam::NFIELDS, rn, glim,
+        nmc_ll_rows_staged(fh, reg, grows + (size_t)ra * Fam::NFIELDS, rn, glim,
                            lrows + (size_t)w * 2 * nmc_stage_buf(Fam::NFIELDS), acc);
       }
 #pragma unroll
@@ -2315,7 +2326,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
 #pragma unroll
           for (int q = 0; q < Fam::MAXP; ++q)
             thp[q] = q < P ? (q == p ? c_prop : th[q * 64]) : 0.0;
-          c_reg = fam.prepare(thp);
+          c_reg = fh.prepare(thp);
         }
         {
           const double na = st[(NMC_ST_NA * P + p) * 64], nr = st[(NMC_ST_NR * P + p) * 64];
@@ -2377,10 +2388,10 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       }
       // the control wave's tiles at the issue priority of the tile waves (its SIMD partner is
       // one of them); the decision after barrier A runs at priority 3 again
-      if (ctl && NMC_CTL_TILE_PRIO && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(0);
+      if (ctl && ctlprio) __builtin_amdgcn_s_setprio(0);
       // ---- likelihood of the proposal (:615-635), tile by tile, every wave ----
       lik_tiles(t, p, sp, [] {});
-      if (ctl && NMC_CTL_TILE_PRIO && !(d.noprio & 1)) __builtin_amdgcn_s_setprio(3);
+      if (ctl && ctlprio) __builtin_amdgcn_s_setprio(3);
       NMC_STAMP(t, 1 + 3 * (p & 1));
       if (ctl || (hl && !pipe && gw)) nmc_drain_vm();   // this wave's LDS-DMA has landed
       NMC_CS(gs - gs0, w);
@@ -2418,6 +2429,11 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       if (ctl) {
         // this step's tiles are all taken; reused at step +2 (from the static entries on)
         if (lane == 0) tcnt[sp] = (unsigned)(nstatic && W > 2 ? W - 2 : 0);
+        if (hl && post_prior) {   // the Gibbs wave evaluated this step's priors (read in the
+                                  // slot sums' LDS round trip)
+          c_lpc = cwv[NMC_CW_LPC * 64];
+          c_lpp = cwv[NMC_CW_LPP * 64];
+        }
         double acc[Fam::NACC];
 #pragma unroll
         for (int j = 0; j < Fam::NACC; ++j) {
@@ -2430,10 +2446,6 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
         const double llp = fh.finish_fast(c_reg, acc, (long)ngrp, gcst);
         if (p == 0) NMC_STAMP(t, 11);
         NMC_CS(gs - gs0, 15);
-        if (hl && post_prior) {   // the Gibbs wave evaluated this step's priors
-          c_lpc = cwv[NMC_CW_LPC * 64];
-          c_lpp = cwv[NMC_CW_LPP * 64];
-        }
         const double postp = c_lpp + llp;
         const double post = c_lpc + c_LL;
         const double diff = postp - post;
@@ -2446,9 +2458,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
         const double vn = accept ? c_prop : c_v;
         th[p * 64] = vn;
         if constexpr (sync) {   // publish write-through; counted at the next step's start
-          if (live)
-            __hip_atomic_store(((t & 1) ? pub1 : pub0) + (size_t)p * G * C, vn,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (live) nmc_store_wt(((t & 1) ? pub1 : pub0) + (size_t)p * G * C, vn);
           if (mb == 0) pub_p = p;   // (row split: member 0 publishes and counts)
         }
         st[(NMC_ST_S * P + p) * 64] = accept ? c_sA : c_sR;
