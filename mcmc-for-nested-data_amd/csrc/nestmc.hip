@@ -741,8 +741,32 @@ int nmc_get_trace(nmc_ctx* x, uint8_t* accept, double* ll_prop) {
   return 0;
 }
 
+// Diagnostics (NMC_TRACE_CALLS=1): host time of nmc_run's / nmc_synchronize's phases, one
+// line per call on stderr (microseconds since the call's entry).
+static const bool g_trace_calls = [] {
+  const char* e = getenv("NMC_TRACE_CALLS");
+  return e && atoi(e) != 0;
+}();
+struct nmc_call_trace {
+  const char* name;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  char buf[256];
+  int n = 0;
+  explicit nmc_call_trace(const char* nm) : name(nm) { buf[0] = 0; }
+  void mark(const char* what) {
+    if (!g_trace_calls) return;
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    n += snprintf(buf + n, sizeof(buf) - n > 0 ? sizeof(buf) - n : 0, " %s %.2f", what, us);
+  }
+  ~nmc_call_trace() {
+    if (g_trace_calls) fprintf(stderr, "[nmc trace] %s:%s\n", name, buf);
+  }
+};
+
 int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
+  nmc_call_trace tr("nmc_run");
   hipSetDevice(x->device);
+  tr.mark("setdev");
   if (!x->scheduled) return fail(-1, "nmc_set_schedule first");
   if (iter_begin < 0 || iter_end < iter_begin) return fail(-1, "invalid iteration range");
   if (iter_begin == iter_end) return 0;
@@ -750,6 +774,7 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
     return fail(-1, "replay variates do not cover the iteration range");
   // a persistent launch that already timed out: stop before queueing more work
   if (int rc0 = check_timeout(x)) return rc0;
+  tr.mark("tmo");
   const bool partial = x->pooling == NMC_POOL_PARTIAL;
   const int P = x->P;
   // the kernels read the values after iteration iter_begin-1 from vb[(iter_begin-1)&1]
@@ -787,6 +812,7 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
         // barrier packet when it is already done)
         if (hipEventQuery(x->pf_ev) != hipSuccess)
           HIPCHK(hipStreamWaitEvent(x->stream, x->pf_ev, 0));
+        tr.mark("pfq");
         if (x->pf.i0 == c0) {
           buf = x->pf.buf;
           have = std::min(c1, x->pf.i1);
@@ -825,6 +851,7 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
         x->d.xbase += (unsigned)steps;
       } else if (x->persistent) {
         if (int rc = launch_run(c0, c1, NMC_RUN_HYPER_LOAD)) return rc;
+        tr.mark("launch");
         x->d.pbase += (unsigned)(c1 - c0);
         x->d.xbase += (unsigned)steps;
       } else {
@@ -833,8 +860,10 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
         if (int rc = launch_hyper(x, c1 - 1)) return rc;   // closes the chunk
       }
       HIPCHK(hipEventRecord(x->rd_ev[buf], x->stream));
+      tr.mark("rdev");
       if (n1 > n0)
         if (int rc = enqueue_prefill(x, n0, n1)) return rc;
+      tr.mark("prefill");
     }
     return 0;
   }();
@@ -866,7 +895,9 @@ int nmc_prefill_stats(nmc_ctx* x, int64_t* issued, int64_t* used) {
 // writers and init threads need them); after that the blocking wait.  NMC_SYNC_POLL_US sets
 // the polling window (0: block at once).
 int nmc_synchronize(nmc_ctx* x) {
+  nmc_call_trace tr("nmc_synchronize");
   hipSetDevice(x->device);
+  int nq = 0;
   static const long poll_us = [] {
     const char* e = getenv("NMC_SYNC_POLL_US");
     return e ? atol(e) : 50000L;
@@ -876,6 +907,7 @@ int nmc_synchronize(nmc_ctx* x) {
   for (hipStream_t s : {x->stream, x->pstream}) {
     for (;;) {
       const hipError_t e = poll_us > 0 ? hipStreamQuery(s) : hipErrorNotReady;
+      ++nq;
       if (e == hipSuccess) break;
       if (e != hipErrorNotReady) return fail(-2, std::string("hipStreamQuery: ") + hipGetErrorString(e));
       const auto dt = std::chrono::steady_clock::now() - t0;
@@ -885,6 +917,12 @@ int nmc_synchronize(nmc_ctx* x) {
       }
       if (dt > std::chrono::microseconds(100)) std::this_thread::yield();
     }
+    tr.mark(s == x->stream ? "stream" : "pstream");
+  }
+  if (g_trace_calls) {
+    char q[32];
+    snprintf(q, sizeof(q), "queries=%d", nq);
+    tr.mark(q);
   }
   return check_timeout(x);
 }
