@@ -751,8 +751,16 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         for (int q = 0; q < MP; ++q)
           if (q == p) thp[q] = prop;
         const typename Fam::Reg reg = fam.prepare(thp);
+        // quad rows ({x, y}, kernels.h nmc_ll_rows_lds_quad): intercept and slope of the four
+        // chains of this lane's quarter position
+        const bool quad = Fam::ASM_ROWS && !HALF && d.quad;
+        double q4c[4], q4d[4];
+        if constexpr (Fam::ASM_ROWS && !HALF) if (quad) {
+          nmc_quarters(reg.b0, q4c);
+          nmc_quarters(reg.b[0], q4d);
+        }
         typename Fam::Reg preg = reg;   // paired rows: the partner lane's (lane ^ 32) values
-        if constexpr (nmc_paired_rows_ok<Fam>() && !HALF) if (d.paired) {
+        if constexpr (nmc_paired_rows_ok<Fam>() && !HALF) if (d.paired && !quad) {
           const bool hi = lane >= 32;
 #pragma unroll
           for (int q = 0; q < MP; ++q) {
@@ -817,7 +825,11 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
             const int ra = v.TI.start(k), rn = v.TI.len(k);
             double acc[Fam::NACC];
             bool done = false;
-            if constexpr (nmc_paired_rows_ok<Fam>()) if (HALF || d.paired) {
+            if constexpr (Fam::ASM_ROWS && !HALF) if (quad) {
+              nmc_ll_rows_lds_quad(fam, reg, lrows + (size_t)ra * NF, rn, acc, q4c, q4d);
+              done = true;
+            }
+            if constexpr (nmc_paired_rows_ok<Fam>()) if (!done && (HALF || d.paired)) {
               nmc_ll_rows_lds<Fam, true, HALF>(fam, reg, lrows + (size_t)ra * NF, rn, acc, &preg);
               done = true;
             }
@@ -1034,7 +1046,6 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
       unsigned* tcnt = (unsigned*)(lds + L.flag * 64 + 4);   // tile queues by step parity
       (void)G; (void)C; (void)tcnt;   // (not every instance uses them)
       const Fam& fam = A->fam;
-      const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
       const int gs = t * P + p, sp = gs & 1;
       const bool due = PARTIAL && gs - v.lag >= v.gs0;   // the Gibbs wave has a task this step
       const bool post_prior = due && P <= 2;             // ... whose update this step's prior needs
@@ -1064,6 +1075,9 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         double naA = na + 1.0, nrA = nr, naR = na, nrR = nr + 1.0;
         c_sA = s;
         c_sR = s;
+        // (the control wave's alone: the burn-in / interval loads and the division stay off
+        //  the other waves' restart)
+        const bool tune = t > 0 && t < d.burn && t % d.tune_interval == 0;
         if (tune) {
           nmc_tune(c_sA, naA, nrA);
           nmc_tune(c_sR, naR, nrR);
@@ -1120,15 +1134,16 @@ nmc_k_sweep(nmc_sweep_args<Fam> a_arg) {
         // every entry is taken; the queue is reused at step gs + 2 (its first nq entries
         // by rank)
         if (lane == 0) tcnt[sp] = (unsigned)(W - 1 - (PARTIAL ? 1 : 0));
+        if (post_prior) {   // the Gibbs wave evaluated this step's priors (read in the slot
+                            // sums' LDS round trip)
+          c_lpc = cwv[NMC_CW_LPC * 64];
+          c_lpp = cwv[NMC_CW_LPP * 64];
+        }
         double acc[Fam::NACC];
 #pragma unroll
         for (int j = 0; j < Fam::NACC; ++j)
           acc[j] = nmc_sum_slots(lds + (L.part + j * NMC_NSLOT) * 64 + lane);
         const double llp = fam.finish_fast(c_reg, acc, (long)v.ngrp, fam.gconst((long)v.ngrp));
-        if (post_prior) {   // the Gibbs wave evaluated this step's priors
-          c_lpc = cwv[NMC_CW_LPC * 64];
-          c_lpp = cwv[NMC_CW_LPP * 64];
-        }
         const double postp = c_lpp + llp;
         const double post = c_lpc + c_LL;
         const double diff = postp - post;

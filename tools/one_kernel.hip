@@ -8,3 +8,7 @@
 template __global__ void nmc_k_run<FamLinreg<2>, NMC_MODE_SYNC_REG, true>(Dev, FamLinreg<2>,
                                                                           const double*, int,
                                                                           int, int);
+#ifdef NMC_ONE_SWEEP   // the cfg-4 step kernel (-DNMC_ONE_SWEEP)
+#include "sweep.h"
+template __global__ void nmc_k_sweep<FamLinreg<2>, NMC_MODE_SYNC_OWN>(nmc_sweep_args<FamLinreg<2>>);
+#endif
