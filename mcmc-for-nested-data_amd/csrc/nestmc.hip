@@ -468,10 +468,12 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
   HIPCHK(hipMemset(d.gfb, 0, 32 * sizeof(unsigned)));
   d.pbase = d.xbase = 0;
   // Dev.gsep: how long the two kernels may take to meet before the likelihood workgroups take
-  // a launch's Gibbs tasks over (NMC_GSEP_PATIENCE_US, default 2 ms); NMC_GSEP_SERIAL (tests)
-  // serializes them on one stream
+  // a launch's Gibbs tasks over (NMC_GSEP_PATIENCE_US, default 20 ms: 2 ms was sometimes too
+  // short for the Gibbs kernel to be dispatched beside a running step kernel and the variate
+  // fill, and a launch fell back while both kernels ran -- the same results, slower);
+  // NMC_GSEP_SERIAL (tests) serializes them on one stream
   d.gep = 0;
-  d.gpat = 200000u;
+  d.gpat = 2000000u;
   if (const char* e = getenv("NMC_GSEP_PATIENCE_US")) d.gpat = (unsigned)(atol(e) * 100);
   x->gserial = getenv("NMC_GSEP_SERIAL") ? atoi(getenv("NMC_GSEP_SERIAL")) : 0;
   // nmc_k_fill's grid: 3 blocks of 256 per CU (its Philox instance's 140 VGPRs: three waves
