@@ -97,6 +97,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="timed window of the CPU baseline sample (0 disables)")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-resident", action="store_true",
+                    help="a new step launch per call (nmc_set_resident off; the A/B)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the two rocprofv3 PMC passes that measure HBM traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -554,6 +556,10 @@ def main():
     # schedule: the warm-up is the burn-in, every measured iteration records a sample row
     n_iter, burn, thin = bench_schedule(W, K)
     eng.set_schedule(n_iter, burn, thin)
+    # the sampling loop's calls share one resident step launch (nmc_set_resident): a call
+    # continuing the last is handed to the running launch, closed as a launch is closed
+    if not args.no_resident:
+        eng.set_resident(True)
     # production launch length: one persistent launch per nmc_run call (up to the
     # variate chunk), exactly as samplePosterior drives the engine -- the warmup is
     # its own launch, the timed region one launch of K iterations
@@ -583,6 +589,7 @@ def main():
     t1 = time.perf_counter()
     barrier()
     pf1 = eng.prefill_stats()
+    res1 = eng.resident_stats()
     # variate fill inside the timed region: iterations drawn on the prefill stream
     # (beside the step launches), iterations taken from the prefill made before it, and the
     # rest drawn on the step stream ahead of their launch
@@ -677,7 +684,11 @@ def main():
                        "parallelism": "chains sharded x%d" % world, "launch": lc,
                        "recorded_iters_in_timed_region": recorded_in(W, W + K, n_iter, burn,
                                                                      thin),
-                       "gibbs_fallbacks": gibbs_fb},
+                       "gibbs_fallbacks": gibbs_fb,
+                       # the timed call ran inside the resident launch the warm-up started
+                       # (its GPU span is event_ms); the kernel-timing pass and the PMC
+                       # passes use separate launches of the same K iterations
+                       "resident": dict(res1, timed_call_resident=res1["calls"] > 0)},
             "roofline": {"bound": "valu", "achieved": valu_tips, "peak": VALU_PEAK_TIPS,
                          "unit": "T fp64 lane-instr/s",
                          "frac": None if valu_tips is None else valu_tips / VALU_PEAK_TIPS,

@@ -135,6 +135,25 @@ int nmc_synchronize(nmc_ctx* ctx);
 int nmc_prefill(nmc_ctx* ctx, int iter_begin, int iter_end);
 /* Iterations drawn by prefills so far / taken by nmc_run from a prefill.      */
 int nmc_prefill_stats(nmc_ctx* ctx, int64_t* issued, int64_t* used);
+/* Resident step launch for the consecutive nmc_run calls of a sampling loop
+ * (Sampler._loop :872-891 driven in chunks, e.g. samplePosterior's progress
+ * steps): a call that continues where the previous one ended is handed to the
+ * running launch (a command word in pinned host memory) instead of a new launch;
+ * the rows and chain state stay in LDS.  Each call is closed as a launch is --
+ * after nmc_synchronize its sample rows, hyper-parameters and state are in HBM,
+ * bit for bit those of separate launches.  Any other entry point parks the
+ * launch first; it parks itself after NMC_RESIDENT_IDLE_US (20 ms) without a
+ * call.  No effect where the context's kernel has no resident form (enabled 0
+ * in nmc_resident_stats).  No reference counterpart: host plumbing.          */
+int nmc_set_resident(nmc_ctx* ctx, int enable);
+/* enabled: resident launches possible and on; active: one is running now;
+ * launches / calls: resident launches made / calls continued inside one;
+ * last_refusal: why the latest call not continued was not (1 another start,
+ * 2 kernel timing, 3 longer than a chunk, 4 past the launch's variate buffer,
+ * 5 variates not prefilled there, 6 counters would wrap, 7 the launch had
+ * parked itself after its idle limit).                                        */
+int nmc_resident_stats(nmc_ctx* ctx, int* enabled, int* active, int64_t* launches,
+                       int64_t* calls, int* last_refusal);
 
 /* Recorded rows [row_begin, row_begin+n_rows) as [row][col][C].
  * Columns follow StepMethod.values / PartialPooling.values (:648-654, :780-787). */

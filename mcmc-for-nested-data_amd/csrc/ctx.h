@@ -41,7 +41,8 @@ struct nmc_ctx {
   double* vzlb[2] = {nullptr, nullptr};
   double* vhb[2] = {nullptr, nullptr};
   int vbuf = 1;                           // buffer of the most recent chunk
-  struct { bool valid; int i0, i1, buf; } pf = {false, 0, 0, 0};
+  // (vb: the iteration at the start of buffer buf -- pf.i0, or a resident launch's first)
+  struct { bool valid; int i0, i1, buf, vb; } pf = {false, 0, 0, 0, 0};
   int prefill_bpc = 1;                    // prefill grid: blocks per CU (beside a step kernel)
   bool prefill_on = true;                 // pipelined fill (NMC_PREFILL=0: off, the A/B)
   long long pf_issued = 0, pf_used = 0;   // iterations prefilled / consumed from a prefill
@@ -81,6 +82,27 @@ struct nmc_ctx {
   double* user_k = nullptr;               // user family: device copy of the model constants
   bool sweep = false;                     // nmc_k_sweep runs the loop (choose_geometry)
   bool no_sweep = false;                  // (its grid could not be resident: nmc_k_run)
+  // Resident launch (nmc_set_resident; kernels.h Dev.rcmd): one step launch serves the
+  // consecutive nmc_run calls of a sampling loop; any other entry point parks it first.
+  struct Resident {
+    bool on = false;                      // requested and possible for this context
+    bool active = false;                  // a resident launch is on the stream
+    unsigned seq = 0;                     // the latest command seq issued
+    unsigned done = 0;                    // the latest seq every workgroup reported done
+    int end = 0;                          // end of the latest call
+    int buf = 0, vbase = 0;               // the variate buffer it reads, its first iteration
+    int nwg = 0;                          // workgroups of the launch
+    void* host = nullptr;                 // pinned block: cmd | ack | done[nwg][4]
+    volatile unsigned long long* cmd = nullptr;
+    volatile unsigned* ack = nullptr;
+    volatile unsigned* done_w = nullptr;
+    unsigned long long* rrel = nullptr;   // device relay word
+    long long launches = 0, calls = 0;    // resident launches / calls continued in one
+    int why = 0;                          // why the latest call was not continued (0: it was)
+    std::vector<std::pair<unsigned, double>> spans;   // (seq, GPU ms) of continued calls
+    bool ev_res[16] = {};                 // event slot recorded as a resident marker
+    unsigned ev_seq[16] = {};
+  } res;
 };
 
 static inline double* vslot(nmc_ctx* x, int slot) { return slot ? x->d.vb1 : x->d.vb0; }
@@ -215,11 +237,13 @@ enum {
   NMC_OP_GROUP_LL = 2,     // in = theta [P][G][C] (device), out = [G][C] (device)
   NMC_OP_OBS_LL = 3,       // in = values [P][G][C] (device), out = [C][n_obs] (device)
   NMC_OP_OBS_LL_ROWS = 4,  // sample rows [i0, i1), chains [c0, c0 + nc) -> out = [nc][i1 - i0][n_obs]
-  NMC_OP_CAPACITY = 5      // result = resident step-kernel workgroups on the device
+  NMC_OP_CAPACITY = 5,     // result = resident step-kernel workgroups on the device
+  NMC_OP_RES_OK = 6        // result = 1: the run mode has a resident instance, grid co-resident
 };
 struct NmcCall {
   int op = 0;
   int i0 = 0, i1 = 0, flags = 0;
+  int res = 0;             // NMC_OP_RUN: the resident instance (Dev.rcmd set)
   int c0 = 0, nc = 0;      // NMC_OP_OBS_LL_ROWS: chains [c0, c0 + nc) (nc = 0: every chain)
   const double* in = nullptr;
   double* out = nullptr;

@@ -24,15 +24,33 @@ template <class Fam>
 static const void* nmc_run_kernel(const nmc_ctx* x, int mode) {
   return x->d.rows_lds ? nmc_run_kernel_rl<Fam, true>(mode) : nmc_run_kernel_rl<Fam, false>(mode);
 }
+// The resident instance (Dev.rcmd: one launch across nmc_run calls) of a mode: rows in LDS,
+// families of <= 3 fields, the modes without a per-launch Gibbs pipeline state beyond the
+// register hand-off (nullptr: none)
+template <class Fam>
+static const void* nmc_run_kernel_res(int mode) {
+  if constexpr (Fam::NFIELDS <= 3) {
+    switch (mode) {
+      case NMC_MODE_NOPOOL: return (const void*)nmc_k_run<Fam, NMC_MODE_NOPOOL, true, true>;
+      case NMC_MODE_SYNC_REG: return (const void*)nmc_k_run<Fam, NMC_MODE_SYNC_REG, true, true>;
+      case NMC_MODE_HALF:
+        if constexpr (nmc_paired_rows_ok<Fam>())
+          return (const void*)nmc_k_run<Fam, NMC_MODE_HALF, true, true>;
+        return nullptr;
+    }
+  }
+  return nullptr;
+}
 
 template <class Fam>
-static int nmc_launch_run(nmc_ctx* x, const Fam& fam, int i0, int i1, int flags) {
+static int nmc_launch_run(nmc_ctx* x, const Fam& fam, int i0, int i1, int flags, bool res) {
   return nmc_run_launches(x, i0, i1, [&](int mode, const Dev& d, dim3 grid, dim3 block,
                                          size_t lds) {
     Dev dd = d;
     const double* obs = d.obs;
     void* args[] = {&dd, (void*)&fam, (void*)&obs, &i0, &i1, &flags};
-    hipLaunchKernel(nmc_run_kernel<Fam>(x, mode), grid, block, args, lds, x->stream);
+    hipLaunchKernel(res ? nmc_run_kernel_res<Fam>(mode) : nmc_run_kernel<Fam>(x, mode), grid,
+                    block, args, lds, x->stream);
   });
 }
 
@@ -53,10 +71,19 @@ template <class Fam>
 static int nmc_fam_call(nmc_ctx* x, const Fam& fam, NmcCall& c) {
   switch (c.op) {
     case NMC_OP_RUN:
-      return nmc_launch_run(x, fam, c.i0, c.i1, c.flags);
+      return nmc_launch_run(x, fam, c.i0, c.i1, c.flags, c.res != 0);
     case NMC_OP_CAN_PERSIST:
       c.result = nmc_can_persist<Fam>(x) ? 1 : 0;
       return 0;
+    case NMC_OP_RES_OK: {   // a resident instance of the run mode, its whole grid co-resident
+      const void* k = x->d.rows_lds ? nmc_run_kernel_res<Fam>(run_mode(x)) : nullptr;
+      int nb = 0;
+      c.result = 0;
+      if (k && hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W,
+                                                            run_lds_bytes(x)) == hipSuccess)
+        c.result = (int64_t)x->d.RB * x->d.G * x->d.S <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
+      return 0;
+    }
     case NMC_OP_CAPACITY: {   // resident step-kernel workgroups of the run mode (safe count)
       int nb = 0;
       const void* k = nmc_run_kernel<Fam>(x, run_mode(x));

@@ -93,6 +93,8 @@ struct Dev {
   int nmax;              // rows of the largest group
   int hlds, naux;        // persistent partial: Gibbs payload via LDS, auxiliary waves
   int hreg;              // persistent partial, G <= 64: Gibbs payload in registers (SYNC_REG)
+  int xpc;               // nmc_k_run, persistent partial pooling, RB | 8: XCDs per chain block
+                         // (workgroup placement, nmc_k_run; 0: chain-block-major)
   unsigned* hrd;         // [RB][P][32] hyper-ready counts of nmc_k_sweep's Gibbs workgroups
                          // (SYNC_OWN; pbase tasks per parameter before)
   int noprio;            // diagnostics: no issue priority for the latency-bound waves
@@ -140,6 +142,20 @@ struct Dev {
   uint8_t* tflag;        // trace [iter][P][G][C]
   double* tllp;
   int trace_n;
+  // Resident launch (nmc_k_run<..., RES = true>; nestmc.hip nmc_set_resident): one launch
+  // serves consecutive nmc_run calls of a sampling loop.  At the end of a call every
+  // workgroup closes it exactly as a launch ends (the last Gibbs tasks, state to HBM, sample
+  // rows), reports it done and waits for the host's next command; workgroup 0 alone reads
+  // the command word in pinned host memory and relays it (rrel) to the others, so all take
+  // the same decision -- a new end, or the park after ridle ticks of s_memrealtime (100 MHz)
+  // without one.  The groups' rows and the chain state stay in LDS between calls.
+  unsigned long long* rcmd;   // pinned host, mapped: (end << 32) | seq; end 0xffffffff = park
+  unsigned long long* rrel;   // device: (end << 32) | relay generation (zeroed per launch)
+  unsigned* rack;        // pinned host: [0] last seq taken, [1] 0x80000000 | seq when parked,
+                         // [2], [3] s_memrealtime when it was taken (lo, hi)
+  unsigned* rdone;       // pinned host: [workgroup][4] {seq done, 0, clock lo, clock hi}
+  unsigned rseq;         // the latest seq the host issued before this launch
+  unsigned ridle;        // idle ticks before workgroup 0 parks the launch
   unsigned long long* stamps;   // diagnostic build only (-DNMC_STAMPS)
 };
 
@@ -262,6 +278,7 @@ __device__ __forceinline__ nmc_pair2 nmc_halves(double v) {
 }
 
 enum { NMC_RUN_HYPER_LOAD = 1 };
+template <bool B> struct nmc_bool_c { static constexpr bool value = B; };
 // Largest step-kernel workgroup (build option): 512 threads = 8 waves, 256 VGPRs per lane;
 // 768 = 12 waves (three per SIMD) caps the kernel at 168 VGPRs.
 #ifndef NMC_RUN_THREADS
@@ -1813,7 +1830,9 @@ __device__ __forceinline__ const Dev* nmc_kdev() {
   return (const Dev*)p;
 }
 
-template <class Fam, int MODE, bool RL = true>
+// RES: the resident launch (Dev.rcmd): iterations [i0, i1) are the first call; later calls
+// extend the end (res_gate below).
+template <class Fam, int MODE, bool RL = true, bool RES = false>
 __global__ void __launch_bounds__(NMC_RUN_THREADS)
 nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, int flags) {
   (void)d_arg;   // (read through nmc_kdev(): the same bytes)
@@ -1840,7 +1859,13 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   const bool nstatic = d.nstatic;
   const bool ctlprio = NMC_CTL_TILE_PRIO && !(d.noprio & 1);
   const int mb = b % S;                           // row-split member (S == 1: 0)
-  const int g = (b / S) % G, cb = (b / S) / G + d.cb0;
+  // (chain block, group) of unit u = b / S: chain-block-major, or (Dev.xpc > 0, S == 1) dealt
+  // so that a chain block's workgroups share xpc XCDs -- blocks b and b + 8 share an XCD
+  // (MI355X_MICROARCH.md, XCD placement) -- and its Gibbs payload is fetched into xpc L2s
+  // rather than all 8.  Placement only: every (chain block, group) computes the same.
+  const int u = b / S, xpc = d.xpc;
+  const int g = xpc ? (u >> 3) * xpc + (u & 7) % xpc : u % G;
+  const int cb = (xpc ? (u & 7) / xpc : u / G) + d.cb0;
   const int c = HALF ? cb * 32 + (lane & 31) : nmc_lane_chain(d, cb, lane);
   // member 0 writes the outputs (half layout: lanes 0-31)
   const bool live = nmc_lane_owns(d, c, lane) && mb == 0 && (!HALF || lane < 32);
@@ -1857,11 +1882,15 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   // counter add, poll -- is behind a whole step) and the priors that need it come from
   // the Gibbs wave when it lands in the step that uses it (P <= 2)
   const int lag = hr && P >= 2 ? 2 : 1;
-  // register mode: the task this workgroup closes after the loop (-1: none)
-  const int close_k = [&]() {
-    const int ge = i1 * P, k0 = ge - lag > i0 * P ? ge - lag : i0 * P;
+  int ie = i1;            // end of the current call (RES: moved by the host's commands)
+  int gfirst = i0 * P;    // first global step of the current call: the Gibbs tasks of the
+                          // steps before it were closed by the launch before / the last gate
+  // register mode: the task this workgroup closes at the end of a call ending at iend (-1:
+  // none) -- tasks ge-lag .. ge-1, task ge-lag+j by the workgroup of group j
+  auto close_of = [&](int iend) {
+    const int ge = iend * P, k0 = ge - lag > gfirst ? ge - lag : gfirst;
     return hr && mb == 0 && k0 + g < ge ? k0 + g : -1;
-  }();
+  };
   // rows in LDS for the launch, or every wave's two staging buffers (nmc_ll_rows_staged)
   const int row_doubles = RL ? d.nmax * Fam::NFIELDS
                              : (Fam::NFIELDS <= 4 ? 0 : nmc_stage_doubles(Fam::NFIELDS, blockDim.x >> 6));
@@ -2077,7 +2106,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     };
     // d.zin: queue entry 0 is the next step's variate job, entries 1.. the tiles
     const int tn = p + 1 < P ? t : t + 1, pn = p + 1 < P ? p + 1 : 0;
-    const int zj = NMC_ZIN_BUILD && d.zin && tn < i1 ? 1 : 0;
+    const int zj = NMC_ZIN_BUILD && d.zin && tn < ie ? 1 : 0;
     // (waves 2.. start on their static entry: one LDS round trip off the step's restart)
     int kq = nstatic && w >= 2 ? (w - 2 < nt + zj ? w - 2 : nt + zj)
                                : (int)__builtin_amdgcn_readlane(grab(), 0);
@@ -2137,7 +2166,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   // update, and (P <= 2) this step's priors; lane 0 leaves the verdict in the flag word
   auto gibbs_step = [&](int t, int p) {
     const int gs = t * P + p;
-    if (gs - lag < i0 * P) return;
+    if (gs - lag < gfirst) return;
     const int k = gs - lag, kq = k % P, kt = k / P;
     NMC_CS(gs - i0 * P, 24);
     const bool r = nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1));
@@ -2175,13 +2204,176 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       NMC_CS(gs - i0 * P, 28);
     }
   };
+  // ---- the state after iteration iend - 1 -> HBM (control wave; the launch's epilogue) ----
+  auto write_state = [&](int iend) {
+    if (!(ctl && live)) return;
+    double* vo = ((iend - 1) & 1) ? d.vb1 : d.vb0;
+    for (int p = 0; p < P; ++p) {
+      const size_t ip = (size_t)p * G * C + gc;
+      if (!sync) vo[ip] = th[p * 64];
+      d.lp[ip] = st[(NMC_ST_LP * P + p) * 64];
+      d.scale[ip] = st[(NMC_ST_S * P + p) * 64];
+      d.nacc[ip] = (int)st[(NMC_ST_NA * P + p) * 64];
+      d.nrej[ip] = (int)st[(NMC_ST_NR * P + p) * 64];
+      d.tacc[ip] = (long long)st[(NMC_ST_TA * P + p) * 64];
+    }
+    d.ll[gc] = c_LL;
+  };
+  // ---- resident launch: the end of a call (t == ie), every wave (uniform) ----
+  // The call is closed as a launch ends -- the last publication counted, the pending step's
+  // state update and sample / trace stores, the state to HBM, the last Gibbs tasks (register
+  // mode: the workgroups of groups 0 .. lag-1, written through and recorded) -- and every
+  // wave's stores drained; then the workgroup reports the call done (pinned host memory) and
+  // takes the next command: workgroup 0 polls the host's command word and relays it, the
+  // others poll the relay.  On a new end: the first step's variates, and every parameter's
+  // hyper-parameters after iteration t - 1 reloaded from HBM as a launch's prologue loads
+  // them (the closing workgroups wrote them), so the next call runs exactly as a new launch
+  // of [t, end) would.  false: the launch ends (park, or a timeout in d.tmo).
+  unsigned rseq = d.rseq;
+  // (GIBBS: the register-mode Gibbs wave's own loop, which runs the closing update; the
+  //  main loop's copy holds no update -- its 64-value payload would be live beside the
+  //  loop's state and raise the kernel's VGPRs past what leaves room for nmc_k_fill's
+  //  prefill wave on each SIMD: 2 x 184 + 144 = 512)
+  auto res_gate = [&](int t, auto gibbs) -> bool {
+    if constexpr (!RES) {
+      (void)t;
+      (void)gibbs;
+      return false;
+    } else {
+      if (ctl) {
+        if constexpr (sync) if (pub_p >= 0) {
+          nmc_drain_vm();
+          if (lane == 0)
+            __hip_atomic_fetch_add(nmc_counter(d, cb, pub_p, g & 7), 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          pub_p = -1;
+        }
+#ifndef XX_NOSTATE
+        if (pend_p >= 0) apply_pending();
+        store_pending();
+        write_state(ie);
+#endif
+      }
+#ifndef XX_NOCLOSE
+      if constexpr (hr) {
+        const int ck = close_of(ie);
+        if (ck >= 0) {
+          const bool pub = nmc_wait_published(d, cb, ck % P,
+                                              (unsigned)G * (unsigned)(ck / P - i0 + 1), lds, L);
+          if constexpr (decltype(gibbs)::value)
+            if (pub) nmc_hyper_update_reg(d, cb, ck / P, ck % P, cc, lds, L.hyp, true);
+        }
+      }
+#endif
+      nmc_drain_vm();
+      __syncthreads();
+      if (ctl) {
+        if (lane == 0) {   // done: the clock, then the seq
+          const unsigned long long clk = __builtin_amdgcn_s_memrealtime();
+          unsigned* dn = d.rdone + (size_t)blockIdx.x * 4;
+          __hip_atomic_store(dn + 2, (unsigned)clk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(dn + 3, (unsigned)(clk >> 32), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+          nmc_drain_vm();
+          __hip_atomic_store(dn, rseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        unsigned end = 0xffffffffu;
+        if (blockIdx.x == 0) {
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          unsigned seq = rseq;
+          for (unsigned spins = 0;; ++spins) {
+            const unsigned long long v =
+                __hip_atomic_load(d.rcmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((int)((unsigned)v - rseq) > 0) {
+              seq = (unsigned)v;
+              end = (unsigned)(v >> 32);
+              break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > d.ridle) break;   // idle: park
+            if ((spins & 63) == 63 &&
+                __hip_atomic_load(d.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+              break;
+            __builtin_amdgcn_s_sleep(4);
+          }
+          // (an idle park relays the next seq: the relay only ever moves forward)
+          __hip_atomic_store(d.rrel,
+                             ((unsigned long long)end << 32) | (seq != rseq ? seq : rseq + 1u),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) {
+            if (seq != rseq && end != 0xffffffffu) {   // taken: the clock, then the seq
+              const unsigned long long clk = __builtin_amdgcn_s_memrealtime();
+              __hip_atomic_store(d.rack + 2, (unsigned)clk, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(d.rack + 3, (unsigned)(clk >> 32), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+              nmc_drain_vm();
+              __hip_atomic_store(d.rack, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {   // parked (idle, or the host's park command seq)
+              __hip_atomic_store(d.rack + 1, 0x80000000u | seq, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+          }
+          rseq = seq;
+        } else {
+          for (unsigned spins = 0;; ++spins) {
+            const unsigned long long v =
+                __hip_atomic_load(d.rrel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((int)((unsigned)v - rseq) > 0) {
+              rseq = (unsigned)v;
+              end = (unsigned)(v >> 32);
+              break;
+            }
+            if ((spins & 255) == 255 &&
+                __hip_atomic_load(d.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+              break;
+            if (spins >= NMC_SPIN_LIMIT) {
+              __hip_atomic_store(d.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+        const bool go = end != 0xffffffffu && (int)end > t;
+        if (go) put_zl(t, 0, (t * P) & 1);   // the first step's {z, log u}
+        if (lane == 0) lds[L.flag * 64 + 2] = go ? (double)end : -1.0;
+      }
+      __syncthreads();
+      const double e = lds[L.flag * 64 + 2];
+      if (e < 0.0) return false;
+#ifndef XX_NORELOAD
+      if constexpr (PARTIAL) {   // hyper-parameters after iteration t - 1 (parameter p by
+                                 // wave p % W, as the prologue)
+        for (int p = w; p < P; p += W) {
+          const size_t ho = nmc_hslot(d, t - 1) + (size_t)p * C + cc;
+          const double s2 = nmc_ldv<NMC_SRC_SC1>(d.s2 + ho);
+          const double m = nmc_ldv<NMC_SRC_SC1>(d.mu + ho);
+          const double sd = nmc_ldv<NMC_SRC_SC1>(d.hsd + ho);
+          const double lsd = nmc_ldv<NMC_SRC_SC1>(d.hlsd + ho);
+          hy[(NMC_HY_MU * P + p) * 64] = m;
+          hy[(NMC_HY_SD * P + p) * 64] = sd;
+          hy[(NMC_HY_LSD * P + p) * 64] = lsd;
+          hy[(NMC_HY_S2 * P + p) * 64] = s2;
+          hy[(NMC_HY_SDM * P + p) * 64] = sqrt(s2 / G);
+          hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sd;
+        }
+      }
+#endif
+      nmc_drain_vm();   // (the control wave's variate DMA has landed)
+      __syncthreads();
+      ie = (int)e;
+      gfirst = t * P;
+      return true;
+    }
+  };
   if constexpr (hr) if (gw) {
     const int gs0 = i0 * P;
-    for (int t = i0; t < i1 && ok; ++t) {
+    (void)gs0;   // (the control-path stamps build)
+    for (int t = i0; ok; ++t) {
+      if (t == ie && !res_gate(t, nmc_bool_c<true>{})) break;
       for (int p = 0; p < P; ++p) {
         dP = nmc_kdev();
         const int gs = t * P + p;
-        const bool due = gs - lag >= gs0;
+        const bool due = gs - lag >= gfirst;
         gibbs_step(t, p);
 #if NMC_GIBBS_TILES   // (A/B build option: the Gibbs wave takes likelihood tiles after its task)
         lik_tiles(t, p, gs & 1, [] {});
@@ -2197,8 +2389,9 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     }
     // closing: tasks ge-lag .. ge-1, task ge-lag+j by the workgroup of group j (member 0),
     // which writes and records it -- in parallel, not one after the other; the same
-    // barrier as the other waves' nmc_wait_published
-    if (ok && close_k >= 0) {
+    // barrier as the other waves' nmc_wait_published (RES: closed at the last gate)
+    const int close_k = close_of(ie);
+    if (!RES && ok && close_k >= 0) {
       if (nmc_wait_published(d, cb, close_k % P, (unsigned)G * (unsigned)(close_k / P - i0 + 1),
                              lds, L))
         nmc_hyper_update_reg(d, cb, close_k / P, close_k % P, cc, lds, L.hyp, true);
@@ -2207,7 +2400,8 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     return;
   }
 
-  for (int t = i0; t < i1 && ok; ++t) {
+  for (int t = i0; ok; ++t) {
+    if (t == ie && !res_gate(t, nmc_bool_c<false>{})) break;
     NMC_STAMP(t, 0);
     for (int p = 0; p < P; ++p) {
       dP = nmc_kdev();
@@ -2233,7 +2427,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       const bool pipe = hl && !hr && P >= 2;   // two-stage (payload-in-LDS) hand-off
       const int aq = p > 0 ? p - 1 : P - 1;        // task gs-1 = (atq, aq)
       const int atq = p > 0 ? t : t - 1;
-      const bool aux_now = hl && gs - lag >= gs0;   // the Gibbs wave's task this step
+      const bool aux_now = hl && gs - lag >= gfirst;   // the Gibbs wave's task this step
       const bool comp_now = pipe && gs - 2 >= gs0;  // Gibbs task gs-2 = (ctq, cq)
       const int cq = (p + 2 * P - 2) % P;
       const int ctq = p >= 2 ? t : t - 1;
@@ -2380,7 +2574,7 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
         store_pending();
         const int tn = p + 1 < P ? t : t + 1;
         const int pn = p + 1 < P ? p + 1 : 0;
-        if (tn < i1 && !(NMC_ZIN_BUILD && d.zin)) put_zl(tn, pn, sp ^ 1);   // (zin: the job)
+        if (tn < ie && !(NMC_ZIN_BUILD && d.zin)) put_zl(tn, pn, sp ^ 1);   // (zin: the job)
       };
       if (ctl) {
         ctl_work();
@@ -2486,6 +2680,10 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   }
 
   NMC_RUN_SL(2);
+  if constexpr (RES) {   // (the last call was closed at its gate)
+    nmc_drain_vm();
+    return;
+  }
   if constexpr (sync) if (ctl && pub_p >= 0) {   // the last parameter's count
     nmc_drain_vm();
     if (lane == 0)
@@ -2496,21 +2694,10 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   if (ctl && pend_p >= 0) apply_pending();
   if (ctl) store_pending();
   // ---- epilogue: state back to HBM (control wave) ----
-  if (ctl && live && ok) {
-    double* vo = ((i1 - 1) & 1) ? d.vb1 : d.vb0;
-    for (int p = 0; p < P; ++p) {
-      const size_t ip = (size_t)p * G * C + gc;
-      if (!sync) vo[ip] = th[p * 64];
-      d.lp[ip] = st[(NMC_ST_LP * P + p) * 64];
-      d.scale[ip] = st[(NMC_ST_S * P + p) * 64];
-      d.nacc[ip] = (int)st[(NMC_ST_NA * P + p) * 64];
-      d.nrej[ip] = (int)st[(NMC_ST_NR * P + p) * 64];
-      d.tacc[ip] = (long long)st[(NMC_ST_TA * P + p) * 64];
-    }
-    d.ll[gc] = c_LL;
-  }
+  if (ok) write_state(i1);
   // ---- closing Gibbs updates after i1-1 (group-0 workgroups write and record them; the
   //      register mode: the workgroups of groups 0 .. lag-1) ----
+  const int close_k = close_of(i1);
   if constexpr (hl) if (ok && (hr ? close_k >= 0 : g0w)) {
     const int ge = i1 * P;   // tasks ge-2 (copied at the last step; P >= 2) and ge-1 are left
     if (!hr && P >= 2 && gw) {

@@ -34,8 +34,14 @@ __device__ __forceinline__ nmc_d2 nmc_fill_hyper(const Dev& d, int it, unsigned 
 // drain dominated, profiles/r05/r05f_fillbench.json).  REPLAY: the replayed reference
 // variates (a separate instance: gammainccinv's registers would cost the Philox fill
 // occupancy).
-template <bool REPLAY>
-__global__ void __launch_bounds__(256) nmc_k_fill(Dev d, int iter0, int T) {
+// MINB: blocks per CU the register budget must allow -- 1 for the fill of the step stream;
+// NMC_FILL_RES_MINB for the prefill beside a resident step launch, which holds two waves
+// per SIMD of up to 208 VGPRs (kernels.h res_gate): 512 - 2 x 208 = 96 VGPRs left per lane
+#ifndef NMC_FILL_RES_MINB
+#define NMC_FILL_RES_MINB 5
+#endif
+template <bool REPLAY, int MINB = 1>
+__global__ void __launch_bounds__(256, MINB) nmc_k_fill(Dev d, int iter0, int T) {
   const unsigned C = (unsigned)d.C, GC = (unsigned)d.G * C, PGC = (unsigned)d.P * GC;
   const unsigned PC = (unsigned)d.P * C;
   const unsigned n1 = d.zin ? 0u : (unsigned)T * PGC;   // (zin: the step kernel draws these)

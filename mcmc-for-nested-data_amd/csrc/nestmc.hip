@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <chrono>
 #include <string>
@@ -269,8 +270,10 @@ static size_t fill_elements(const nmc_ctx* x, int T) {
   const bool partial = x->pooling == NMC_POOL_PARTIAL;
   return (size_t)T * x->P * x->C * ((x->d.zin ? 0 : x->G) + (partial ? 1 : 0));
 }
-// nmc_k_fill of iterations [a, b) into buffer buf, whose first iteration is vb
-static int launch_fill(nmc_ctx* x, int buf, int vb, int a, int b, hipStream_t s, int bpc) {
+// nmc_k_fill of iterations [a, b) into buffer buf, whose first iteration is vb (beside: the
+// instance whose waves fit beside a resident step launch's, kernels_misc.h NMC_FILL_RES_MINB)
+static int launch_fill(nmc_ctx* x, int buf, int vb, int a, int b, hipStream_t s, int bpc,
+                       bool beside = false) {
   const size_t n = fill_elements(x, b - a);
   if (!n) return 0;
   Dev df = x->d;
@@ -282,6 +285,9 @@ static int launch_fill(nmc_ctx* x, int buf, int vb, int a, int b, hipStream_t s,
   const int blocks = (int)std::min<int64_t>((int64_t)((n + 255) / 256), cap);
   if (x->rng == NMC_RNG_REPLAY)
     hipLaunchKernelGGL(nmc_k_fill<true>, dim3(blocks), dim3(256), 0, s, df, a, b - a);
+  else if (beside)
+    hipLaunchKernelGGL((nmc_k_fill<false, NMC_FILL_RES_MINB>), dim3(blocks), dim3(256), 0, s, df,
+                       a, b - a);
   else
     hipLaunchKernelGGL(nmc_k_fill<false>, dim3(blocks), dim3(256), 0, s, df, a, b - a);
   HIPCHK(hipGetLastError());
@@ -299,8 +305,155 @@ static int enqueue_prefill(nmc_ctx* x, int a, int b) {
   x->pf.i0 = a;
   x->pf.i1 = b;
   x->pf.buf = buf;
+  x->pf.vb = a;
   x->pf_issued += b - a;
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Resident launch (nmc_set_resident).  A call of a sampling loop that continues where the
+// resident launch's last call ended, fits its variate buffer and finds its variates
+// prefilled there is handed to the running launch as a command (pinned host memory) instead
+// of a new launch: no dispatch, no prologue (rows and chain state stay in LDS), no closing
+// beyond the call's own.  Each call is still closed completely at its end (kernels.h
+// res_gate): when nmc_synchronize returns, its sample rows, hyper-parameters and state are
+// in HBM exactly as after a launch of that call.  Every other entry point parks the launch
+// first; workgroup 0 parks it by itself after NMC_RESIDENT_IDLE_US (20 ms) without a call.
+// ---------------------------------------------------------------------------
+static bool res_kernel_gone(nmc_ctx* x) { return hipStreamQuery(x->stream) == hipSuccess; }
+
+// wait until every workgroup reported the latest seq done; record the call's GPU span
+static int res_wait_done(nmc_ctx* x) {
+  auto& r = x->res;
+  if (!r.active || r.done == r.seq) return 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  int b = 0;
+  for (unsigned long spins = 0;; ++spins) {
+    while (b < r.nwg && r.done_w[4 * b] == r.seq) ++b;
+    if (b == r.nwg) break;
+    if ((spins & 1023) == 1023) {
+      if (*x->tmo_host) {
+        r.active = false;
+        hipStreamSynchronize(x->stream);
+        return check_timeout(x);
+      }
+      if (res_kernel_gone(x)) {
+        r.active = false;
+        return fail(-5, "resident launch ended before its call completed");
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100))
+        std::this_thread::yield();
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  // GPU span: workgroup 0 taking the command -> the last workgroup done (s_memrealtime)
+  if (r.ack[0] == r.seq) {
+    const unsigned long long a = ((unsigned long long)r.ack[3] << 32) | r.ack[2];
+    unsigned long long e = 0;
+    for (int k = 0; k < r.nwg; ++k)
+      e = std::max(e, ((unsigned long long)r.done_w[4 * k + 3] << 32) | r.done_w[4 * k + 2]);
+    r.spans.emplace_back(r.seq, e >= a ? (double)(e - a) / 1e5 : -1.0);
+    if (r.spans.size() > 64) r.spans.erase(r.spans.begin(), r.spans.begin() + 32);
+  }
+  r.done = r.seq;
+  return 0;
+}
+
+// end the resident launch (park command) and wait for it (its pending prefill stays: a
+// launch starting there reads it at its offset, Dev.vbase = pf.vb)
+static int res_park(nmc_ctx* x) {
+  auto& r = x->res;
+  if (!r.active) return 0;
+  hipSetDevice(x->device);
+  const unsigned seq = r.seq + 1;
+  *r.cmd = (0xffffffffull << 32) | seq;
+  r.seq = seq;
+  r.done = seq;
+  r.active = false;
+  HIPCHK(hipStreamSynchronize(x->stream));
+  return check_timeout(x);
+}
+#define RES_PARK(x)                          \
+  do {                                       \
+    if (int rc_ = res_park(x)) return rc_;   \
+  } while (0)
+
+// prefill of iterations [a, b) into the resident launch's buffer, at their offset from its
+// first iteration (the launch reads other iterations of the same buffer: no wait)
+static int res_prefill(nmc_ctx* x, int a, int b) {
+  auto& r = x->res;
+  b = std::min(b, r.vbase + x->d.vcap);
+  if (b <= a) return 0;
+  if (int rc = launch_fill(x, r.buf, r.vbase, a, b, x->pstream, x->prefill_bpc, true)) return rc;
+  HIPCHK(hipEventRecord(x->pf_ev, x->pstream));
+  x->pf.valid = true;
+  x->pf.i0 = a;
+  x->pf.i1 = b;
+  x->pf.buf = r.buf;
+  x->pf.vb = r.vbase;
+  x->pf_issued += b - a;
+  return 0;
+}
+
+// nmc_run's iterations [i0, i1) as the resident launch's next call: 1 taken, 0 not
+// possible (the launch is parked: the caller launches), < 0 error
+static int res_continue(nmc_ctx* x, int i0, int i1) {
+  auto& r = x->res;
+  // why a call is not continued (nmc_resident_stats): 1 another start, 2 kernel timing,
+  // 3 longer than a chunk, 4 past the launch's variate buffer, 5 its variates not prefilled
+  // there, 6 the counters would wrap, 7 the launch had parked itself (idle)
+  const int why = i0 != r.end ? 1 : x->ktiming ? 2 : i1 - i0 > fill_chunk(x) ? 3
+                : i1 - r.vbase > x->d.vcap ? 4
+                : !(x->pf.valid && x->pf.buf == r.buf && x->pf.i0 == i0 && x->pf.i1 >= i1) ? 5
+                : ((uint64_t)x->G * (x->d.pbase + (uint64_t)(i1 - i0)) >= (1ull << 31) ||
+                   (uint64_t)x->d.S * (x->d.xbase + (uint64_t)(i1 - i0) * x->P) >= (1ull << 31))
+                    ? 6 : 0;
+  if (why) {
+    r.why = why;
+    RES_PARK(x);
+    return 0;
+  }
+  if (int rc = res_wait_done(x)) return rc;
+  // the call's variates have landed (the prefill stream is not the launch's)
+  if (hipEventQuery(x->pf_ev) != hipSuccess) HIPCHK(hipEventSynchronize(x->pf_ev));
+  const unsigned seq = r.seq + 1;
+  *r.cmd = ((unsigned long long)(unsigned)i1 << 32) | seq;
+  r.seq = seq;
+  // taken, or workgroup 0 parked (idle) before it saw the command
+  for (unsigned long spins = 0;; ++spins) {
+    if (r.ack[0] == seq) break;
+    if (r.ack[1] == (0x80000000u | (seq - 1))) {
+      r.why = 7;
+      r.done = seq;
+      r.active = false;
+      HIPCHK(hipStreamSynchronize(x->stream));
+      if (int rc = check_timeout(x)) return rc;
+      return 0;
+    }
+    if ((spins & 1023) == 1023) {
+      if (*x->tmo_host) return check_timeout(x);
+      if (res_kernel_gone(x) && r.ack[0] != seq &&
+          r.ack[1] != (0x80000000u | (seq - 1))) {
+        r.active = false;
+        return fail(-5, "resident launch ended without taking or refusing a call");
+      }
+    }
+  }
+  x->pf_used += i1 - i0;
+  x->pf.valid = false;
+  r.end = i1;
+  r.calls += 1;
+  x->d.pbase += (unsigned)(i1 - i0);
+  x->d.xbase += (unsigned)((i1 - i0) * x->P);
+  x->cur_slot = (i1 - 1) & 1;
+  // the next call's variates beside this one (the same length, while the schedule and the
+  // buffer last)
+  if (x->prefill_on) {
+    const int n1 = std::min({i1 + (i1 - i0), x->n_iter, r.vbase + x->d.vcap});
+    if (n1 > i1)
+      if (int rc = res_prefill(x, i1, n1)) return rc;
+  }
+  return 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -539,6 +692,14 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     // of chain blocks when the whole grid is not (chain blocks are independent)
     x->persistent = c.result == 1 || d.S > 1;
   }
+  // XCD-aware placement of nmc_k_run's persistent partial-pooling grid (Dev.xpc): the RB
+  // chain blocks on 8 / RB XCDs each, when RB divides 8 and the groups split evenly
+  // (NMC_XMAP=0: chain-block-major, the A/B)
+  d.xpc = 0;
+  if (pooling == NMC_POOL_PARTIAL && x->persistent && !x->sweep && d.S == 1 && d.RB <= 8 &&
+      8 % d.RB == 0 && n_groups % (8 / d.RB) == 0 &&
+      !(getenv("NMC_XMAP") && atoi(getenv("NMC_XMAP")) == 0))
+    d.xpc = 8 / d.RB;
   if (d.S > 1) {   // row split: resident batches of chain blocks, exchange buffers
     NmcCall c;
     c.op = NMC_OP_CAPACITY;
@@ -583,6 +744,7 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
 int nmc_destroy(nmc_ctx* x) {
   if (!x) return 0;
   hipSetDevice(x->device);
+  res_park(x);
   if (x->stream) hipStreamSynchronize(x->stream);
   if (x->gstream) hipStreamSynchronize(x->gstream);
   if (x->pstream) hipStreamSynchronize(x->pstream);
@@ -597,12 +759,14 @@ int nmc_destroy(nmc_ctx* x) {
   if (x->gstream) hipStreamDestroy(x->gstream);
   if (x->stream) hipStreamDestroy(x->stream);
   if (x->tmo_host) hipHostFree((void*)x->tmo_host);
+  if (x->res.host) hipHostFree(x->res.host);
   delete x;
   return 0;
 }
 
 int nmc_set_state(nmc_ctx* x, const double* value, const double* log_prior, const double* ll,
                   const double* hyper_mu, const double* hyper_sigma2, const double* scale) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   Dev& d = x->d;
   const size_t PGC = (size_t)x->P * x->G * x->C, GC = (size_t)x->G * x->C, PC = (size_t)x->P * x->C;
@@ -634,6 +798,7 @@ int nmc_set_state(nmc_ctx* x, const double* value, const double* log_prior, cons
 
 int nmc_get_state(nmc_ctx* x, double* value, double* log_prior, double* ll, double* hyper_mu,
                   double* hyper_sigma2, double* scale) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   HIPCHK(hipStreamSynchronize(x->stream));
   Dev& d = x->d;
@@ -650,6 +815,7 @@ int nmc_get_state(nmc_ctx* x, double* value, double* log_prior, double* ll, doub
 
 int nmc_set_replay(nmc_ctx* x, const double* z, const double* u, const double* hz,
                    const double* hu, int n_iter) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   Dev& d = x->d;
   const size_t n = (size_t)n_iter * x->P * x->G * x->C, nh = (size_t)n_iter * x->P * x->C;
@@ -682,6 +848,7 @@ static int alloc_trace(nmc_ctx* x) {
 }
 
 int nmc_set_schedule(nmc_ctx* x, int n_iter, int burn, int thin, int tune_interval) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   if (n_iter < 0 || burn < 0 || burn > n_iter || thin < 1 || tune_interval < 1)
     return fail(-1, "invalid schedule");
@@ -728,12 +895,14 @@ int nmc_n_rows(nmc_ctx* x, int* rows, int* cols) {
 }
 
 int nmc_set_trace(nmc_ctx* x, int enable) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   x->trace = enable != 0;
   return alloc_trace(x);
 }
 
 int nmc_get_trace(nmc_ctx* x, uint8_t* accept, double* ll_prop) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   HIPCHK(hipStreamSynchronize(x->stream));
   if (!x->d.trace_n) return fail(-1, "trace not enabled");
@@ -777,6 +946,12 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
   // a persistent launch that already timed out: stop before queueing more work
   if (int rc0 = check_timeout(x)) return rc0;
   tr.mark("tmo");
+  if (x->res.active) {   // the next call of the resident launch, or park it
+    const int rc = res_continue(x, iter_begin, iter_end);
+    tr.mark("resident");
+    if (rc < 0) return rc;
+    if (rc == 1) return 0;
+  }
   const bool partial = x->pooling == NMC_POOL_PARTIAL;
   const int P = x->P;
   // the kernels read the values after iteration iter_begin-1 from vb[(iter_begin-1)&1]
@@ -792,12 +967,13 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
     }
     x->cur_slot = need;
   }
-  auto launch_run = [&](int i0, int i1, int flags) -> int {
+  auto launch_run = [&](int i0, int i1, int flags, bool res = false) -> int {
     NmcCall c;
     c.op = NMC_OP_RUN;
     c.i0 = i0;
     c.i1 = i1;
     c.flags = flags;
+    c.res = res ? 1 : 0;
     return nmc_call_family(x, c);
   };
   int rc = [&]() -> int {
@@ -808,15 +984,18 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       // every variate of iterations [c0, c1) before the chunk's step launch: the hyper
       // variates (partial pooling) and the step variates (unless the step kernel draws them),
       // from the pending prefill where it starts at c0, the rest in one fully parallel launch
-      int buf = x->vbuf ^ 1, have = c0;
+      int buf = x->vbuf ^ 1, have = c0, vb = c0;
       if (x->pf.valid) {
         // (whatever it holds, the prefill's writes end before this stream goes on; no
         // barrier packet when it is already done)
         if (hipEventQuery(x->pf_ev) != hipSuccess)
           HIPCHK(hipStreamWaitEvent(x->stream, x->pf_ev, 0));
         tr.mark("pfq");
-        if (x->pf.i0 == c0) {
+        // (a prefill into a resident launch's buffer sits at its offset from that launch's
+        // first iteration pf.vb: usable while the chunk fits the buffer from there)
+        if (x->pf.i0 == c0 && c1 - x->pf.vb <= x->d.vcap) {
           buf = x->pf.buf;
+          vb = x->pf.vb;
           have = std::min(c1, x->pf.i1);
           x->pf_used += have - c0;
         }
@@ -825,9 +1004,9 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       x->vbuf = buf;
       x->d.vzl = x->vzlb[buf];
       x->d.vh = x->vhb[buf];
-      x->d.vbase = c0;
+      x->d.vbase = vb;
       if (fills && have < c1)
-        if (int rc = launch_fill(x, buf, c0, have, c1, x->stream, x->fill_bpc)) return rc;
+        if (int rc = launch_fill(x, buf, vb, have, c1, x->stream, x->fill_bpc)) return rc;
       // the next chunk's variates beside this chunk's step launch (enqueued after it): the
       // rest of this call, or the same length again after it (the next call of a sampling
       // loop) while the schedule lasts
@@ -848,7 +1027,28 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
                                 x->stream));
         x->d.pbase = x->d.xbase = 0;
       }
-      if (!partial) {
+      // a one-chunk call of a resident context: the resident instance, which then takes the
+      // following calls (res_continue)
+      const bool resl = x->res.on && !x->ktiming && c0 == iter_begin && c1 == iter_end &&
+                        (!partial || x->persistent);
+      if (resl) {
+        auto& r = x->res;
+        HIPCHK(hipMemsetAsync(r.rrel, 0, sizeof(unsigned long long), x->stream));
+        r.ack[1] = 0;
+        r.seq += 1;
+        r.done = r.seq - 1;
+        x->d.rseq = r.seq;
+        if (int rc = launch_run(c0, c1, partial ? NMC_RUN_HYPER_LOAD : 0, true)) return rc;
+        tr.mark("launch");
+        r.active = true;
+        r.end = c1;
+        r.buf = buf;
+        r.vbase = vb;
+        r.nwg = x->d.RB * x->G * x->d.S;
+        r.launches += 1;
+        x->d.pbase += (unsigned)(c1 - c0);
+        x->d.xbase += (unsigned)steps;
+      } else if (!partial) {
         if (int rc = launch_run(c0, c1, 0)) return rc;
         x->d.xbase += (unsigned)steps;
       } else if (x->persistent) {
@@ -863,8 +1063,13 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
       }
       HIPCHK(hipEventRecord(x->rd_ev[buf], x->stream));
       tr.mark("rdev");
-      if (n1 > n0)
-        if (int rc = enqueue_prefill(x, n0, n1)) return rc;
+      if (n1 > n0) {
+        if (resl) {   // into the resident launch's buffer, after this call's iterations
+          if (int rc = res_prefill(x, n0, n1)) return rc;
+        } else if (int rc = enqueue_prefill(x, n0, n1)) {
+          return rc;
+        }
+      }
       tr.mark("prefill");
     }
     return 0;
@@ -881,6 +1086,11 @@ int nmc_prefill(nmc_ctx* x, int iter_begin, int iter_end) {
   if (x->rng == NMC_RNG_REPLAY && (!x->d.rz || iter_end > x->d.replay_n))
     return fail(-1, "replay variates do not cover the iteration range");
   if (iter_begin == iter_end || !x->prefill_on || fill_elements(x, 1) == 0) return 0;
+  if (x->res.active) {   // the resident launch's next call: into its buffer
+    if (iter_begin == x->res.end && iter_end - x->res.vbase <= x->d.vcap)
+      return res_prefill(x, iter_begin, iter_end);
+    RES_PARK(x);
+  }
   return enqueue_prefill(x, iter_begin, iter_end);
 }
 
@@ -905,8 +1115,14 @@ int nmc_synchronize(nmc_ctx* x) {
     return e ? atol(e) : 50000L;
   }();
   const auto t0 = std::chrono::steady_clock::now();
+  // a resident launch: every workgroup reports the latest call done (the launch itself stays)
+  if (x->res.active) {
+    if (int rc = res_wait_done(x)) return rc;
+    tr.mark("resident");
+  }
   // the step stream, then the prefill stream (a prefill is part of the work a call enqueued)
   for (hipStream_t s : {x->stream, x->pstream}) {
+    if (s == x->stream && x->res.active) continue;
     for (;;) {
       const hipError_t e = poll_us > 0 ? hipStreamQuery(s) : hipErrorNotReady;
       ++nq;
@@ -930,6 +1146,7 @@ int nmc_synchronize(nmc_ctx* x) {
 }
 
 int nmc_get_samples(nmc_ctx* x, int row_begin, int n_rows, double* out) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   const Dev& d = x->d;
   if (row_begin < 0 || n_rows < 0 || row_begin + n_rows > d.n_rows)
@@ -944,6 +1161,7 @@ int nmc_get_samples(nmc_ctx* x, int row_begin, int n_rows, double* out) {
 }
 
 int nmc_get_accept_counts(nmc_ctx* x, int64_t* out) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   HIPCHK(hipStreamSynchronize(x->stream));
   HIPCHK(hipMemcpy(out, x->d.tacc, (size_t)x->P * x->G * x->C * 8, hipMemcpyDeviceToHost));
@@ -951,6 +1169,7 @@ int nmc_get_accept_counts(nmc_ctx* x, int64_t* out) {
 }
 
 int nmc_eval_group_ll(nmc_ctx* x, const double* theta, double* out) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   const size_t PGC = (size_t)x->P * x->G * x->C, GC = (size_t)x->G * x->C;
   double *th = nullptr, *o = nullptr, *part = nullptr;
@@ -977,6 +1196,7 @@ int nmc_eval_group_ll(nmc_ctx* x, const double* theta, double* out) {
 }
 
 int nmc_eval_obs_ll(nmc_ctx* x, double* out) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   const size_t n = (size_t)x->C * x->n_obs;
   double* o = nullptr;
@@ -996,28 +1216,111 @@ int nmc_eval_obs_ll(nmc_ctx* x, double* out) {
   return rc;
 }
 
+// With a resident launch on the stream an event would complete only when the launch ends:
+// the slot marks the latest call issued instead, and the elapsed time between two marks is
+// the sum of the GPU spans (s_memrealtime: workgroup 0 taking the call -> the last workgroup
+// done) of the calls issued between them.
 int nmc_event_record(nmc_ctx* x, int slot) {
   if (slot < 0 || slot >= 16) return fail(-1, "event slot 0..15");
   hipSetDevice(x->device);
-  HIPCHK(hipEventRecord(x->ev[slot], x->stream));
+  x->res.ev_res[slot] = x->res.active;
+  x->res.ev_seq[slot] = x->res.seq;
+  if (!x->res.active) HIPCHK(hipEventRecord(x->ev[slot], x->stream));
   return 0;
 }
 
 int nmc_event_elapsed(nmc_ctx* x, int a, int b, float* ms) {
   if (a < 0 || a >= 16 || b < 0 || b >= 16) return fail(-1, "event slot 0..15");
   hipSetDevice(x->device);
+  auto& r = x->res;
+  if (r.ev_res[a] || r.ev_res[b]) {
+    if (!(r.ev_res[a] && r.ev_res[b]))
+      return fail(-1, "event slots on both sides of a resident launch's start or park");
+    if ((int)(r.ev_seq[b] - r.done) > 0)
+      if (int rc = res_wait_done(x)) return rc;
+    double sum = 0;
+    for (unsigned q = r.ev_seq[a] + 1; (int)(r.ev_seq[b] - q) >= 0; ++q) {
+      auto it = std::find_if(r.spans.begin(), r.spans.end(),
+                             [&](const std::pair<unsigned, double>& e) { return e.first == q; });
+      if (it == r.spans.end() || it->second < 0)
+        return fail(-1, "no GPU span for a call between the event slots (the launch's first "
+                        "call, or a parked one)");
+      sum += it->second;
+    }
+    *ms = (float)sum;
+    return 0;
+  }
   HIPCHK(hipEventSynchronize(x->ev[b]));
   HIPCHK(hipEventElapsedTime(ms, x->ev[a], x->ev[b]));
   return 0;
 }
 
+int nmc_set_resident(nmc_ctx* x, int enable) {
+  hipSetDevice(x->device);
+  auto& r = x->res;
+  if (!enable) {
+    RES_PARK(x);
+    r.on = false;
+    return 0;
+  }
+  if (r.on) return 0;
+  // possible: a built-in family on nmc_k_run with the rows in LDS, one member per group,
+  // drawn (not replayed) variates from the fill, and a resident instance of the run mode
+  // whose whole grid is co-resident
+  if (x->family >= NMC_LL_USER_BASE || x->sweep || x->rng == NMC_RNG_REPLAY || x->d.zin ||
+      !x->d.rows_lds || x->d.S != 1 ||
+      (x->pooling == NMC_POOL_PARTIAL && !x->persistent))
+    return 0;
+  NmcCall c;
+  c.op = NMC_OP_RES_OK;
+  if (int rc = nmc_call_family(x, c)) return rc;
+  if (c.result != 1) return 0;
+  if (!r.host) {
+    const int nwg = x->d.RB * x->G * x->d.S;
+    const size_t bytes = 256 + (size_t)16 * nwg;
+    void* h = nullptr;
+    void* dp = nullptr;
+    HIPCHK(hipHostMalloc(&h, bytes, hipHostMallocCoherent | hipHostMallocMapped));
+    memset(h, 0, bytes);
+    r.host = h;
+    if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess)
+      return fail(-2, "resident launch: pinned command block not mapped");
+    r.cmd = (volatile unsigned long long*)h;
+    r.ack = (volatile unsigned*)((char*)h + 128);
+    r.done_w = (volatile unsigned*)((char*)h + 256);
+    x->d.rcmd = (unsigned long long*)dp;
+    x->d.rack = (unsigned*)((char*)dp + 128);
+    x->d.rdone = (unsigned*)((char*)dp + 256);
+    if (int rc = dalloc(x, &r.rrel, 16)) return rc;
+    x->d.rrel = r.rrel;
+  }
+  // workgroup 0 parks the launch after this long without a call (NMC_RESIDENT_IDLE_US)
+  const char* e = getenv("NMC_RESIDENT_IDLE_US");
+  x->d.ridle = (unsigned)std::min(4.0e9, 100.0 * (e ? atof(e) : 20000.0));
+  r.on = true;
+  return 0;
+}
+
+int nmc_resident_stats(nmc_ctx* x, int* enabled, int* active, int64_t* launches, int64_t* calls,
+                       int* last_refusal) {
+  if (last_refusal) *last_refusal = x->res.why;
+  if (enabled) *enabled = x->res.on ? 1 : 0;
+  if (active) *active = x->res.active ? 1 : 0;
+  if (launches) *launches = x->res.launches;
+  if (calls) *calls = x->res.calls;
+  return 0;
+}
+
+
 int nmc_set_launch_iters(nmc_ctx* x, int max_iters) {
+  RES_PARK(x);
   if (max_iters < 0) return fail(-1, "max_iters < 0");
   x->launch_iters = max_iters;
   return 0;
 }
 
 int nmc_set_kernel_timing(nmc_ctx* x, int enable) {
+  if (enable) RES_PARK(x);   // (per-launch events: the timed launches are not resident)
   x->ktiming = enable != 0;
   x->kev_used = x->hev_used = 0;
   x->step_ms = x->hyper_ms = 0;
@@ -1085,6 +1388,7 @@ int nmc_kernel_name(nmc_ctx* x, char* out, int cap) {
 }
 
 int nmc_gibbs_fallbacks(nmc_ctx* x, int64_t* out) {
+  RES_PARK(x);
   if (!out) return fail(-1, "gibbs fallbacks: null output");
   hipSetDevice(x->device);
   HIPCHK(hipStreamSynchronize(x->stream));
@@ -1167,6 +1471,7 @@ static int ensure_gidx(nmc_ctx* x) {
 }
 
 int nmc_obs_ll_rows(nmc_ctx* x, int row_begin, int n_rows, double* out) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   if (row_begin < 0 || n_rows < 0 || row_begin + n_rows > x->d.n_rows || n_rows > 65535)
     return fail(-1, "row range out of bounds (at most 65535 rows per call)");
@@ -1199,6 +1504,7 @@ int nmc_obs_ll_rows(nmc_ctx* x, int row_begin, int n_rows, double* out) {
 // every chain within a 256 MiB budget, or -- when one row of every chain exceeds it
 // (many chains x many observations) -- one row of a sub-range of the chains.
 int nmc_write_ll_csvs(nmc_ctx* x, const char* dir, const int32_t* chain_ids, int threads) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   HIPCHK(hipStreamSynchronize(x->stream));
   if (int rc = check_timeout(x)) return rc;
@@ -1362,6 +1668,7 @@ int nmc_comm_size(void* comm, int* nranks, int* rank) {
 
 int nmc_gather_samples(nmc_ctx* x, void* comm, int root, double* host_out,
                        int64_t host_capacity) {
+  RES_PARK(x);
   hipSetDevice(x->device);
   ncclComm_t c = (ncclComm_t)comm;
   int nranks = 0, rank = 0;
@@ -1405,6 +1712,7 @@ int nmc_debug_prior_logpdf(int fam, const double* prm8, const double* xs, int n,
 // Diagnostic build only: (re)allocate and zero the stamp buffer (n > 0) and/or copy
 // it back (out != NULL): NMC_STAMP_WORDS uint64 (kernels.h NMC_STAMP / NMC_CS layouts).
 int nmc_debug_stamps(nmc_ctx* x, int n, uint64_t* out) {
+  RES_PARK(x);
 #if defined(NMC_STAMPS) || defined(NMC_CSTAMPS)
   hipSetDevice(x->device);
   if (n > 0) {

@@ -54,6 +54,9 @@ SIGNATURES = {
     "nmc_prefill": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
     "nmc_prefill_stats": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64),
                                          ctypes.POINTER(ctypes.c_int64)]),
+    "nmc_set_resident": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "nmc_resident_stats": (ctypes.c_int, [_vp, _c_int_p, _c_int_p, _c_int64_p, _c_int64_p,
+                                          _c_int_p]),
     "nmc_get_samples": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _c_double_p]),
     "nmc_get_accept_counts": (ctypes.c_int, [_vp, _c_int64_p]),
     "nmc_eval_group_ll": (ctypes.c_int, [_vp, _c_double_p, _c_double_p]),

@@ -138,6 +138,20 @@ class Engine:
         check(self.lib.nmc_prefill_stats(self.h, ctypes.byref(a), ctypes.byref(b)))
         return {"issued": a.value, "used": b.value}
 
+    def set_resident(self, on=True):
+        """One step launch for consecutive run() calls (nmc_set_resident): a call continuing
+        the last is handed to the running launch.  Results are bit-identical either way."""
+        check(self.lib.nmc_set_resident(self.h, 1 if on else 0))
+
+    def resident_stats(self):
+        """{"enabled", "active", "launches", "calls", "last_refusal"} (nmc_resident_stats)."""
+        e, a, w = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        n, c = ctypes.c_int64(), ctypes.c_int64()
+        check(self.lib.nmc_resident_stats(self.h, ctypes.byref(e), ctypes.byref(a),
+                                          ctypes.byref(n), ctypes.byref(c), ctypes.byref(w)))
+        return {"enabled": bool(e.value), "active": bool(a.value), "launches": n.value,
+                "calls": c.value, "last_refusal": w.value}
+
     # -- results --------------------------------------------------------------
     def samples_raw(self, row_begin=0, n_rows=None):
         """[rows][cols][C] exactly as stored on the device."""

@@ -293,6 +293,12 @@ def _sample_loop(engines, nIter, burn, thin, names, G, partial, saveLogLikelihoo
     t_loop = datetime.datetime.now()
     steps = 10 if displayProgress and nIter >= 10 else 1
     bounds = [round(nIter * k / steps) for k in range(steps + 1)]
+    # the progress steps' calls continue one another: each engine's calls share one resident
+    # step launch (nmc_set_resident; bit-identical) when the engine has its device to itself
+    devs = [eng.device for eng, _, _ in engines]
+    if steps > 1 and len(set(devs)) == len(devs):
+        for eng, _, _ in engines:
+            eng.set_resident(True)
     for k in range(steps):
         for eng, _, _ in engines:
             eng.run(bounds[k], bounds[k + 1])

@@ -89,10 +89,13 @@ def partial_state(fam, sizes, C, P, seed=11, spread=1.0):
 
 
 def run_engine(fam, sizes, st, sel, chain_base, n_iter, seed, pooling="partial", priors=None,
-               env=None, burn=None, thin=1, tune_interval=5, launch_iters=0, calls=None):
+               env=None, burn=None, thin=1, tune_interval=5, launch_iters=0, calls=None,
+               resident=False):
     """Run the HIP engine on chains ``sel`` of state ``st``; returns
     (accept flags [C, iter, P, G], proposal LLs, recorded rows [C, rows, cols], launch config).
-    calls: the engine calls in order, ("run" | "prefill", i0, i1) (default: one run)."""
+    calls: the engine calls in order, ("run" | "prefill", i0, i1), ("synchronize", 0, 0),
+    ("sleep", ms, 0) or ("get_state", 0, 0) (default: one run).  resident: nmc_set_resident
+    (launch config: "resident" stats, "state" the final get_state, "accept" the counts)."""
     import os
     from nestmc.engine import Engine
     old = {}
@@ -115,13 +118,28 @@ def run_engine(fam, sizes, st, sel, chain_base, n_iter, seed, pooling="partial",
     eng.set_trace(True)
     if launch_iters:
         eng.set_launch_iters(launch_iters)
+    if resident:
+        eng.set_resident(True)
     for op, a, b in calls or [("run", 0, n_iter)]:
-        getattr(eng, op)(a, b)
+        if op == "synchronize":
+            eng.synchronize()
+        elif op == "sleep":
+            import time
+            time.sleep(a / 1e3)
+        elif op == "get_state":
+            eng.get_state()
+        else:
+            getattr(eng, op)(a, b)
+    eng.synchronize()
+    res = eng.resident_stats()
     acc, llp = eng.trace(n_iter)
     rows = eng.samples()
     cfg = eng.launch_config()
     cfg["gibbs_fallbacks"] = eng.gibbs_fallbacks()
     cfg["prefill"] = eng.prefill_stats()
+    cfg["resident"] = res
+    cfg["state"] = eng.get_state()
+    cfg["accept"] = eng.accept_counts()
     eng.close()
     return acc, llp, rows, cfg
 

@@ -55,3 +55,36 @@ def test_save_loglikelihood_matches_reference(gpu_lib, tmp_path):
     assert lines[-1] == m["ll0_last"]
     assert hashlib.sha256(raw).hexdigest() == m["ll0_sha256"]
     assert filecmp.cmp(os.path.join(out, "sample", "sample.0.csv"), c.csv_path(0), shallow=False)
+
+
+@pytest.mark.parametrize("name", ["linreg_partial", "regression_none"])
+def test_progress_steps_resident_byte_identical(gpu_lib, name, tmp_path, monkeypatch):
+    """displayProgress=True drives the loop in ten calls (posteriorSampling.py:872-891 with
+    its progress prints), which share one resident step launch (nmc_set_resident): the
+    sample files are byte for byte those of the one-call run on the Philox stream."""
+    from nestmc.engine import Engine
+    if name not in CASES:
+        pytest.skip("no such golden case")
+    c = Case(name)
+    stats = []
+    close = Engine.close
+
+    def close_and_record(self):
+        if getattr(self, "h", None):
+            stats.append(self.resident_stats())
+        close(self)
+
+    monkeypatch.setattr(Engine, "close", close_and_record)
+    outs = []
+    for progress in (False, True):
+        out = str(tmp_path / ("p%d" % progress)) + "/"
+        sample_posterior(c.n_chains, c.n_iter, c.n_samples, c.names, c.n_groups, c.n_per_group,
+                         c.pooling, family_for(c), out, saveLogLikelihood=False,
+                         priorDistribution=c.priors, startWithMLE=c.mle,
+                         startingPointValueRange=c.ranges, displayProgress=progress, seed=5)
+        outs.append(out)
+    assert stats[0]["launches"] == 0, stats
+    assert stats[-1]["enabled"] and stats[-1]["calls"] >= 1, stats
+    for ch in range(c.n_chains):
+        a, b = (os.path.join(o, "sample", "sample.%i.csv" % ch) for o in outs)
+        assert filecmp.cmp(a, b, shallow=False), (name, ch)

@@ -12,3 +12,7 @@ template __global__ void nmc_k_run<FamLinreg<2>, NMC_MODE_SYNC_REG, true>(Dev, F
 #include "sweep.h"
 template __global__ void nmc_k_sweep<FamLinreg<2>, NMC_MODE_SYNC_OWN>(nmc_sweep_args<FamLinreg<2>>);
 #endif
+#ifdef NMC_ONE_RES   // the resident cfg-3 step kernel (-DNMC_ONE_RES)
+template __global__ void nmc_k_run<FamLinreg<2>, NMC_MODE_SYNC_REG, true, true>(
+    Dev, FamLinreg<2>, const double*, int, int, int);
+#endif
