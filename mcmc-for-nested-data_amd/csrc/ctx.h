@@ -92,13 +92,14 @@ struct nmc_ctx {
     int end = 0;                          // end of the latest call
     int buf = 0, vbase = 0;               // the variate buffer it reads, its first iteration
     int nwg = 0;                          // workgroups of the launch
-    void* host = nullptr;                 // pinned block: cmd | ack | done[nwg][4]
+    void* host = nullptr;                 // pinned block: cmd | ack | done
     volatile unsigned long long* cmd = nullptr;
     volatile unsigned* ack = nullptr;
     volatile unsigned* done_w = nullptr;
-    unsigned long long* rrel = nullptr;   // device relay word
+    unsigned* rsync = nullptr;            // device: relay, done count, clocks (Dev.rsync)
     long long launches = 0, calls = 0;    // resident launches / calls continued in one
     int why = 0;                          // why the latest call was not continued (0: it was)
+    int fill_minb = 1;                    // nmc_k_fill instance that fits beside the launch
     std::vector<std::pair<unsigned, double>> spans;   // (seq, GPU ms) of continued calls
     bool ev_res[16] = {};                 // event slot recorded as a resident marker
     unsigned ev_seq[16] = {};
@@ -249,6 +250,7 @@ struct NmcCall {
   double* out = nullptr;
   double* aux = nullptr;   // op-specific device scratch
   int result = 0;
+  int result2 = 0;         // NMC_OP_RES_OK: the resident instance's VGPRs per lane
 };
 int nmc_call_linreg(nmc_ctx* x, NmcCall& c);
 int nmc_call_gauss_mean(nmc_ctx* x, NmcCall& c);

@@ -82,6 +82,8 @@ static int nmc_fam_call(nmc_ctx* x, const Fam& fam, NmcCall& c) {
       if (k && hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 64 * x->d.W,
                                                             run_lds_bytes(x)) == hipSuccess)
         c.result = (int64_t)x->d.RB * x->d.G * x->d.S <= (int64_t)nmc_safe_blocks(x, nb) * x->ncu;
+      hipFuncAttributes fa{};
+      c.result2 = k && hipFuncGetAttributes(&fa, k) == hipSuccess ? fa.numRegs : 0;   // VGPRs
       return 0;
     }
     case NMC_OP_CAPACITY: {   // resident step-kernel workgroups of the run mode (safe count)

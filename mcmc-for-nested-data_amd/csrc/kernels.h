@@ -144,16 +144,21 @@ struct Dev {
   int trace_n;
   // Resident launch (nmc_k_run<..., RES = true>; nestmc.hip nmc_set_resident): one launch
   // serves consecutive nmc_run calls of a sampling loop.  At the end of a call every
-  // workgroup closes it exactly as a launch ends (the last Gibbs tasks, state to HBM, sample
-  // rows), reports it done and waits for the host's next command; workgroup 0 alone reads
-  // the command word in pinned host memory and relays it (rrel) to the others, so all take
-  // the same decision -- a new end, or the park after ridle ticks of s_memrealtime (100 MHz)
-  // without one.  The groups' rows and the chain state stay in LDS between calls.
+  // workgroup completes its results as a launch does (the last Gibbs tasks, sample rows),
+  // counts itself done and waits for the host's next command; workgroup 0 alone reads the
+  // command word in pinned host memory and relays it (rsync) to the others, so all take the
+  // same decision -- a new end, or the park after ridle ticks of s_memrealtime (100 MHz)
+  // without one.  The groups' rows and the chain state stay in LDS between calls; the state
+  // goes to HBM when the launch parks.
   unsigned long long* rcmd;   // pinned host, mapped: (end << 32) | seq; end 0xffffffff = park
-  unsigned long long* rrel;   // device: (end << 32) | relay generation (zeroed per launch)
+  unsigned* rsync;       // device, zeroed per launch: the relay (end << 32) | seq, one copy
+                         // per XCD line (NMC_RSYNC_REL + 32 k), the done count (NMC_RSYNC_CNT)
+                         // and the calls' start / loop-end clock maxima (NMC_RSYNC_MAX, u64)
   unsigned* rack;        // pinned host: [0] last seq taken, [1] 0x80000000 | seq when parked,
                          // [2], [3] s_memrealtime when it was taken (lo, hi)
-  unsigned* rdone;       // pinned host: [workgroup][4] {seq done, 0, clock lo, clock hi}
+  unsigned* rdone;       // pinned host, written by the last workgroup done: {seq done, 0, then
+                         // the s_memrealtime (lo, hi) of: done, the latest loop end, the
+                         // latest start of the call}
   unsigned rseq;         // the latest seq the host issued before this launch
   unsigned ridle;        // idle ticks before workgroup 0 parks the launch
   unsigned long long* stamps;   // diagnostic build only (-DNMC_STAMPS)
@@ -279,6 +284,8 @@ __device__ __forceinline__ nmc_pair2 nmc_halves(double v) {
 
 enum { NMC_RUN_HYPER_LOAD = 1 };
 template <bool B> struct nmc_bool_c { static constexpr bool value = B; };
+// Dev.rsync word offsets (u32): relay lines, done counter, clock maxima; 512 words in all
+enum { NMC_RSYNC_REL = 0, NMC_RSYNC_CNT = 256, NMC_RSYNC_MAX = 288, NMC_RSYNC_WORDS = 512 };
 // Largest step-kernel workgroup (build option): 512 threads = 8 waves, 256 VGPRs per lane;
 // 768 = 12 waves (three per SIMD) caps the kernel at 168 VGPRs.
 #ifndef NMC_RUN_THREADS
@@ -2220,26 +2227,29 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     d.ll[gc] = c_LL;
   };
   // ---- resident launch: the end of a call (t == ie), every wave (uniform) ----
-  // The call is closed as a launch ends -- the last publication counted, the pending step's
-  // state update and sample / trace stores, the state to HBM, the last Gibbs tasks (register
-  // mode: the workgroups of groups 0 .. lag-1, written through and recorded) -- and every
-  // wave's stores drained; then the workgroup reports the call done (pinned host memory) and
-  // takes the next command: workgroup 0 polls the host's command word and relays it, the
-  // others poll the relay.  On a new end: the first step's variates, and every parameter's
-  // hyper-parameters after iteration t - 1 reloaded from HBM as a launch's prologue loads
-  // them (the closing workgroups wrote them), so the next call runs exactly as a new launch
-  // of [t, end) would.  false: the launch ends (park, or a timeout in d.tmo).
-  unsigned rseq = d.rseq;
+  // The call's results are completed as a launch completes them -- the last publication
+  // counted, the pending step's state update and sample / trace stores, the call's last Gibbs
+  // tasks (register mode: by every workgroup's Gibbs wave for its own hyper state, as the
+  // in-loop tasks are; group 0's writes them through and records them) -- and every wave's
+  // stores drained; the workgroup counts itself done (the last one of the grid tells the
+  // host: pinned memory) and takes the next command: workgroup 0 polls the host's command
+  // word and relays it, the others poll the relay of their XCD.  On a new end: the first
+  // step's variates; the Gibbs pipeline restarts as at a launch's start (gfirst), so the next
+  // call runs exactly as a new launch of [t, end) would.  The chain state (values, scales,
+  // counters, priors, group LLs) stays in LDS and is written to HBM when the launch parks.
+  // false: the launch ends (park, or a timeout in d.tmo).
+  unsigned rseq = d.rseq, rcall = 0;   // (rcall: calls of this launch done)
+  // (s_memrealtime when this workgroup started the current call: reported with its done)
+  unsigned long long rt_start = RES ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // (GIBBS: the register-mode Gibbs wave's own loop, which runs the closing update; the
-  //  main loop's copy holds no update -- its 64-value payload would be live beside the
-  //  loop's state and raise the kernel's VGPRs past what leaves room for nmc_k_fill's
-  //  prefill wave on each SIMD: 2 x 184 + 144 = 512)
+  //  main loop's copy holds no update and no 64-value payload)
   auto res_gate = [&](int t, auto gibbs) -> bool {
     if constexpr (!RES) {
       (void)t;
       (void)gibbs;
       return false;
     } else {
+      const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();   // the call's loop done
       if (ctl) {
         if constexpr (sync) if (pub_p >= 0) {
           nmc_drain_vm();
@@ -2248,34 +2258,52 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
                                    __HIP_MEMORY_SCOPE_AGENT);
           pub_p = -1;
         }
-#ifndef XX_NOSTATE
         if (pend_p >= 0) apply_pending();
         store_pending();
-        write_state(ie);
-#endif
       }
-#ifndef XX_NOCLOSE
-      if constexpr (hr) {
-        const int ck = close_of(ie);
-        if (ck >= 0) {
-          const bool pub = nmc_wait_published(d, cb, ck % P,
-                                              (unsigned)G * (unsigned)(ck / P - i0 + 1), lds, L);
-          if constexpr (decltype(gibbs)::value)
-            if (pub) nmc_hyper_update_reg(d, cb, ck / P, ck % P, cc, lds, L.hyp, true);
+      // the call's last Gibbs tasks, by every workgroup's Gibbs wave for its own hyper state
+      // as the in-loop tasks are (group 0's writes and records them)
+      if constexpr (hr && decltype(gibbs)::value) {
+        const int ge = ie * P;
+        for (int k = ge - lag > gfirst ? ge - lag : gfirst; k < ge; ++k) {
+          const int kq = k % P, kt = k / P;
+          if (!nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1))) break;
+          // keep the payload loads below the poll (no instruction: wavefront scope)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          nmc_hyper_update_reg(d, cb, kt, kq, cc, lds, L.hyp, g0w);
         }
       }
-#endif
       nmc_drain_vm();
       __syncthreads();
       if (ctl) {
-        if (lane == 0) {   // done: the clock, then the seq
-          const unsigned long long clk = __builtin_amdgcn_s_memrealtime();
-          unsigned* dn = d.rdone + (size_t)blockIdx.x * 4;
-          __hip_atomic_store(dn + 2, (unsigned)clk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(dn + 3, (unsigned)(clk >> 32), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane == 0) {
+          // done: this workgroup's start / loop-end clocks into the launch's maxima, then its
+          // arrival on the device counter; the last of the grid tells the host (one write
+          // to pinned memory per call, not one per workgroup: PCIe writes are the slow part)
+          unsigned long long* mx = (unsigned long long*)(d.rsync + NMC_RSYNC_MAX);
+          __hip_atomic_fetch_max(mx, rt_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_max(mx + 1, rt_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           nmc_drain_vm();
-          __hip_atomic_store(dn, rseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          rcall += 1;
+          const unsigned n = __hip_atomic_fetch_add(d.rsync + NMC_RSYNC_CNT, 1u,
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (n + 1 == rcall * gridDim.x) {
+            const unsigned long long ck[3] = {
+                __builtin_amdgcn_s_memrealtime(),
+                __hip_atomic_load(mx + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                __hip_atomic_load(mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
+            __hip_atomic_store(mx, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(mx + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              __hip_atomic_store(d.rdone + 2 + 2 * k, (unsigned)ck[k], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(d.rdone + 3 + 2 * k, (unsigned)(ck[k] >> 32), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            nmc_drain_vm();
+            __hip_atomic_store(d.rdone, rseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
         }
         unsigned end = 0xffffffffu;
         if (blockIdx.x == 0) {
@@ -2295,10 +2323,13 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
               break;
             __builtin_amdgcn_s_sleep(4);
           }
-          // (an idle park relays the next seq: the relay only ever moves forward)
-          __hip_atomic_store(d.rrel,
-                             ((unsigned long long)end << 32) | (seq != rseq ? seq : rseq + 1u),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // (an idle park relays the next seq: the relay only ever moves forward); one copy
+          // per XCD's workgroups (b & 7), each on its own 128-B line: 32 pollers a line
+          if (lane < 8)
+            __hip_atomic_store(
+                (unsigned long long*)(d.rsync + NMC_RSYNC_REL + 32 * lane),
+                ((unsigned long long)end << 32) | (seq != rseq ? seq : rseq + 1u),
+                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (lane == 0) {
             if (seq != rseq && end != 0xffffffffu) {   // taken: the clock, then the seq
               const unsigned long long clk = __builtin_amdgcn_s_memrealtime();
@@ -2317,7 +2348,9 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
         } else {
           for (unsigned spins = 0;; ++spins) {
             const unsigned long long v =
-                __hip_atomic_load(d.rrel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_load((unsigned long long*)(d.rsync + NMC_RSYNC_REL +
+                                                        32 * (blockIdx.x & 7)),
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if ((int)((unsigned)v - rseq) > 0) {
               rseq = (unsigned)v;
               end = (unsigned)(v >> 32);
@@ -2340,52 +2373,39 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       __syncthreads();
       const double e = lds[L.flag * 64 + 2];
       if (e < 0.0) return false;
-#ifndef XX_NORELOAD
-      if constexpr (PARTIAL) {   // hyper-parameters after iteration t - 1 (parameter p by
-                                 // wave p % W, as the prologue)
-        for (int p = w; p < P; p += W) {
-          const size_t ho = nmc_hslot(d, t - 1) + (size_t)p * C + cc;
-          const double s2 = nmc_ldv<NMC_SRC_SC1>(d.s2 + ho);
-          const double m = nmc_ldv<NMC_SRC_SC1>(d.mu + ho);
-          const double sd = nmc_ldv<NMC_SRC_SC1>(d.hsd + ho);
-          const double lsd = nmc_ldv<NMC_SRC_SC1>(d.hlsd + ho);
-          hy[(NMC_HY_MU * P + p) * 64] = m;
-          hy[(NMC_HY_SD * P + p) * 64] = sd;
-          hy[(NMC_HY_LSD * P + p) * 64] = lsd;
-          hy[(NMC_HY_S2 * P + p) * 64] = s2;
-          hy[(NMC_HY_SDM * P + p) * 64] = sqrt(s2 / G);
-          hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sd;
-        }
-      }
-#endif
       nmc_drain_vm();   // (the control wave's variate DMA has landed)
       __syncthreads();
       ie = (int)e;
       gfirst = t * P;
+      rt_start = __builtin_amdgcn_s_memrealtime();
       return true;
     }
   };
   if constexpr (hr) if (gw) {
     const int gs0 = i0 * P;
     (void)gs0;   // (the control-path stamps build)
-    for (int t = i0; ok; ++t) {
-      if (t == ie && !res_gate(t, nmc_bool_c<true>{})) break;
-      for (int p = 0; p < P; ++p) {
-        dP = nmc_kdev();
-        const int gs = t * P + p;
-        const bool due = gs - lag >= gfirst;
-        gibbs_step(t, p);
+    // (calls: the steps of [t, ie), then -- resident launch -- the gate to the next call,
+    //  outside the step loop: its Gibbs updates then share no live range with the loop's)
+    for (int t = i0;;) {
+      for (; t < ie && ok; ++t) {
+        for (int p = 0; p < P; ++p) {
+          dP = nmc_kdev();
+          const int gs = t * P + p;
+          const bool due = gs - lag >= gfirst;
+          gibbs_step(t, p);
 #if NMC_GIBBS_TILES   // (A/B build option: the Gibbs wave takes likelihood tiles after its task)
-        lik_tiles(t, p, gs & 1, [] {});
+          lik_tiles(t, p, gs & 1, [] {});
 #endif
-        NMC_CS(gs - gs0, w);
-        nmc_run_barrier();   // A
-        if (due) {
-          ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
-          if (!ok) break;
+          NMC_CS(gs - gs0, w);
+          nmc_run_barrier();   // A
+          if (due) {
+            ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
+            if (!ok) break;
+          }
+          nmc_run_barrier();   // B
         }
-        nmc_run_barrier();   // B
       }
+      if (!ok || !res_gate(t, nmc_bool_c<true>{})) break;
     }
     // closing: tasks ge-lag .. ge-1, task ge-lag+j by the workgroup of group j (member 0),
     // which writes and records it -- in parallel, not one after the other; the same
@@ -2680,7 +2700,8 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   }
 
   NMC_RUN_SL(2);
-  if constexpr (RES) {   // (the last call was closed at its gate)
+  if constexpr (RES) {   // (the last call was closed at its gate): the state to HBM
+    if (ok) write_state(ie);
     nmc_drain_vm();
     return;
   }

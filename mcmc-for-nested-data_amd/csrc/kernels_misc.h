@@ -34,12 +34,10 @@ __device__ __forceinline__ nmc_d2 nmc_fill_hyper(const Dev& d, int it, unsigned 
 // drain dominated, profiles/r05/r05f_fillbench.json).  REPLAY: the replayed reference
 // variates (a separate instance: gammainccinv's registers would cost the Philox fill
 // occupancy).
-// MINB: blocks per CU the register budget must allow -- 1 for the fill of the step stream;
-// NMC_FILL_RES_MINB for the prefill beside a resident step launch, which holds two waves
-// per SIMD of up to 208 VGPRs (kernels.h res_gate): 512 - 2 x 208 = 96 VGPRs left per lane
-#ifndef NMC_FILL_RES_MINB
-#define NMC_FILL_RES_MINB 5
-#endif
+// MINB: blocks per CU (waves per SIMD) the register budget must allow -- 1 for the fill of
+// the step stream (140 VGPRs); 4, 5, 6 or 8 (128, 96, 80, 64 VGPRs, with spills) for the prefill
+// beside a resident step launch, whatever fits the VGPRs its waves leave on each SIMD
+// (nestmc.hip nmc_set_resident): a fill that does not fit would wait for the launch to end
 template <bool REPLAY, int MINB = 1>
 __global__ void __launch_bounds__(256, MINB) nmc_k_fill(Dev d, int iter0, int T) {
   const unsigned C = (unsigned)d.C, GC = (unsigned)d.G * C, PGC = (unsigned)d.P * GC;

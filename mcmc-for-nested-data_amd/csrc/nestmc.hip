@@ -285,9 +285,14 @@ static int launch_fill(nmc_ctx* x, int buf, int vb, int a, int b, hipStream_t s,
   const int blocks = (int)std::min<int64_t>((int64_t)((n + 255) / 256), cap);
   if (x->rng == NMC_RNG_REPLAY)
     hipLaunchKernelGGL(nmc_k_fill<true>, dim3(blocks), dim3(256), 0, s, df, a, b - a);
-  else if (beside)
-    hipLaunchKernelGGL((nmc_k_fill<false, NMC_FILL_RES_MINB>), dim3(blocks), dim3(256), 0, s, df,
-                       a, b - a);
+  else if (beside && x->res.fill_minb == 4)
+    hipLaunchKernelGGL((nmc_k_fill<false, 4>), dim3(blocks), dim3(256), 0, s, df, a, b - a);
+  else if (beside && x->res.fill_minb == 5)
+    hipLaunchKernelGGL((nmc_k_fill<false, 5>), dim3(blocks), dim3(256), 0, s, df, a, b - a);
+  else if (beside && x->res.fill_minb == 6)
+    hipLaunchKernelGGL((nmc_k_fill<false, 6>), dim3(blocks), dim3(256), 0, s, df, a, b - a);
+  else if (beside && x->res.fill_minb == 8)
+    hipLaunchKernelGGL((nmc_k_fill<false, 8>), dim3(blocks), dim3(256), 0, s, df, a, b - a);
   else
     hipLaunchKernelGGL(nmc_k_fill<false>, dim3(blocks), dim3(256), 0, s, df, a, b - a);
   HIPCHK(hipGetLastError());
@@ -310,6 +315,28 @@ static int enqueue_prefill(nmc_ctx* x, int a, int b) {
   return 0;
 }
 
+// Diagnostics (NMC_TRACE_CALLS=1): host time of nmc_run's / nmc_synchronize's phases, one
+// line per call on stderr (microseconds since the call's entry).
+static const bool g_trace_calls = [] {
+  const char* e = getenv("NMC_TRACE_CALLS");
+  return e && atoi(e) != 0;
+}();
+struct nmc_call_trace {
+  const char* name;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  char buf[256];
+  int n = 0;
+  explicit nmc_call_trace(const char* nm) : name(nm) { buf[0] = 0; }
+  void mark(const char* what) {
+    if (!g_trace_calls) return;
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    n += snprintf(buf + n, sizeof(buf) - n > 0 ? sizeof(buf) - n : 0, " %s %.2f", what, us);
+  }
+  ~nmc_call_trace() {
+    if (g_trace_calls) fprintf(stderr, "[nmc trace] %s:%s\n", name, buf);
+  }
+};
+
 // ---------------------------------------------------------------------------
 // Resident launch (nmc_set_resident).  A call of a sampling loop that continues where the
 // resident launch's last call ended, fits its variate buffer and finds its variates
@@ -327,10 +354,8 @@ static int res_wait_done(nmc_ctx* x) {
   auto& r = x->res;
   if (!r.active || r.done == r.seq) return 0;
   const auto t0 = std::chrono::steady_clock::now();
-  int b = 0;
   for (unsigned long spins = 0;; ++spins) {
-    while (b < r.nwg && r.done_w[4 * b] == r.seq) ++b;
-    if (b == r.nwg) break;
+    if (r.done_w[0] == r.seq) break;
     if ((spins & 1023) == 1023) {
       if (*x->tmo_host) {
         r.active = false;
@@ -348,11 +373,16 @@ static int res_wait_done(nmc_ctx* x) {
   std::atomic_thread_fence(std::memory_order_acquire);
   // GPU span: workgroup 0 taking the command -> the last workgroup done (s_memrealtime)
   if (r.ack[0] == r.seq) {
+    auto clk = [&](int j) {
+      return ((unsigned long long)r.done_w[3 + 2 * j] << 32) | r.done_w[2 + 2 * j];
+    };
     const unsigned long long a = ((unsigned long long)r.ack[3] << 32) | r.ack[2];
-    unsigned long long e = 0;
-    for (int k = 0; k < r.nwg; ++k)
-      e = std::max(e, ((unsigned long long)r.done_w[4 * k + 3] << 32) | r.done_w[4 * k + 2]);
+    const unsigned long long e = clk(0), le = clk(1), st = clk(2);
     r.spans.emplace_back(r.seq, e >= a ? (double)(e - a) / 1e5 : -1.0);
+    if (g_trace_calls)   // (the critical path: the last workgroup to start, to end its loop)
+      fprintf(stderr, "[nmc trace] resident call %u: relay %.2f loop %.2f close %.2f us\n",
+              r.seq, ((double)st - (double)a) / 100.0, ((double)le - (double)st) / 100.0,
+              ((double)e - (double)le) / 100.0);
     if (r.spans.size() > 64) r.spans.erase(r.spans.begin(), r.spans.begin() + 32);
   }
   r.done = r.seq;
@@ -414,8 +444,20 @@ static int res_continue(nmc_ctx* x, int i0, int i1) {
     return 0;
   }
   if (int rc = res_wait_done(x)) return rc;
-  // the call's variates have landed (the prefill stream is not the launch's)
-  if (hipEventQuery(x->pf_ev) != hipSuccess) HIPCHK(hipEventSynchronize(x->pf_ev));
+  // the call's variates have landed (the prefill runs beside the launch, which it fits:
+  // nmc_set_resident); a prefill not done within 2 ms parks the launch rather than wait
+  // for its idle limit -- whatever held the fill back, it cannot start beside the launch
+  {
+    const auto tq = std::chrono::steady_clock::now();
+    while (hipEventQuery(x->pf_ev) != hipSuccess) {
+      if (std::chrono::steady_clock::now() - tq > std::chrono::milliseconds(2)) {
+        r.why = 8;
+        RES_PARK(x);
+        return 0;
+      }
+      std::this_thread::yield();
+    }
+  }
   const unsigned seq = r.seq + 1;
   *r.cmd = ((unsigned long long)(unsigned)i1 << 32) | seq;
   r.seq = seq;
@@ -692,13 +734,13 @@ int nmc_create(nmc_ctx** out, int device, int n_chains, int chain_base, int n_gr
     // of chain blocks when the whole grid is not (chain blocks are independent)
     x->persistent = c.result == 1 || d.S > 1;
   }
-  // XCD-aware placement of nmc_k_run's persistent partial-pooling grid (Dev.xpc): the RB
-  // chain blocks on 8 / RB XCDs each, when RB divides 8 and the groups split evenly
-  // (NMC_XMAP=0: chain-block-major, the A/B)
+  // XCD-aware placement of nmc_k_run's persistent partial-pooling grid (Dev.xpc, NMC_XMAP=1):
+  // the RB chain blocks on 8 / RB XCDs each, when RB divides 8 and the groups split evenly.
+  // Measured 1.5-2.5 % slower at cfg 3 than chain-block-major (profiles/r06/r06n_*): off
   d.xpc = 0;
   if (pooling == NMC_POOL_PARTIAL && x->persistent && !x->sweep && d.S == 1 && d.RB <= 8 &&
-      8 % d.RB == 0 && n_groups % (8 / d.RB) == 0 &&
-      !(getenv("NMC_XMAP") && atoi(getenv("NMC_XMAP")) == 0))
+      8 % d.RB == 0 && n_groups % (8 / d.RB) == 0 && getenv("NMC_XMAP") &&
+      atoi(getenv("NMC_XMAP")) == 1)
     d.xpc = 8 / d.RB;
   if (d.S > 1) {   // row split: resident batches of chain blocks, exchange buffers
     NmcCall c;
@@ -912,28 +954,6 @@ int nmc_get_trace(nmc_ctx* x, uint8_t* accept, double* ll_prop) {
   return 0;
 }
 
-// Diagnostics (NMC_TRACE_CALLS=1): host time of nmc_run's / nmc_synchronize's phases, one
-// line per call on stderr (microseconds since the call's entry).
-static const bool g_trace_calls = [] {
-  const char* e = getenv("NMC_TRACE_CALLS");
-  return e && atoi(e) != 0;
-}();
-struct nmc_call_trace {
-  const char* name;
-  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-  char buf[256];
-  int n = 0;
-  explicit nmc_call_trace(const char* nm) : name(nm) { buf[0] = 0; }
-  void mark(const char* what) {
-    if (!g_trace_calls) return;
-    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-    n += snprintf(buf + n, sizeof(buf) - n > 0 ? sizeof(buf) - n : 0, " %s %.2f", what, us);
-  }
-  ~nmc_call_trace() {
-    if (g_trace_calls) fprintf(stderr, "[nmc trace] %s:%s\n", name, buf);
-  }
-};
-
 int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
   nmc_call_trace tr("nmc_run");
   hipSetDevice(x->device);
@@ -1033,7 +1053,7 @@ int nmc_run(nmc_ctx* x, int iter_begin, int iter_end) {
                         (!partial || x->persistent);
       if (resl) {
         auto& r = x->res;
-        HIPCHK(hipMemsetAsync(r.rrel, 0, sizeof(unsigned long long), x->stream));
+        HIPCHK(hipMemsetAsync(r.rsync, 0, NMC_RSYNC_WORDS * sizeof(unsigned), x->stream));
         r.ack[1] = 0;
         r.seq += 1;
         r.done = r.seq - 1;
@@ -1275,9 +1295,19 @@ int nmc_set_resident(nmc_ctx* x, int enable) {
   c.op = NMC_OP_RES_OK;
   if (int rc = nmc_call_family(x, c)) return rc;
   if (c.result != 1) return 0;
+  if (g_trace_calls)
+    fprintf(stderr, "[nmc trace] resident instance: %d VGPRs\n", c.result2);
+  // the prefill's fill beside the launch: the largest instance that fits the VGPRs the
+  // launch's waves leave per SIMD lane (512; allocation granule 8), else none fits
+  {
+    const int wps = (x->d.W + 3) / 4;   // the launch's waves per SIMD
+    const int left = 512 - wps * ((c.result2 + 7) / 8) * 8;
+    r.fill_minb = left >= 144 ? 1 : left >= 128 ? 4 : left >= 96 ? 5 : left >= 80 ? 6
+                : left >= 64 ? 8 : 0;
+    if (!r.fill_minb) return 0;
+  }
   if (!r.host) {
-    const int nwg = x->d.RB * x->G * x->d.S;
-    const size_t bytes = 256 + (size_t)16 * nwg;
+    const size_t bytes = 512;
     void* h = nullptr;
     void* dp = nullptr;
     HIPCHK(hipHostMalloc(&h, bytes, hipHostMallocCoherent | hipHostMallocMapped));
@@ -1291,8 +1321,8 @@ int nmc_set_resident(nmc_ctx* x, int enable) {
     x->d.rcmd = (unsigned long long*)dp;
     x->d.rack = (unsigned*)((char*)dp + 128);
     x->d.rdone = (unsigned*)((char*)dp + 256);
-    if (int rc = dalloc(x, &r.rrel, 16)) return rc;
-    x->d.rrel = r.rrel;
+    if (int rc = dalloc(x, &r.rsync, NMC_RSYNC_WORDS)) return rc;
+    x->d.rsync = r.rsync;
   }
   // workgroup 0 parks the launch after this long without a call (NMC_RESIDENT_IDLE_US)
   const char* e = getenv("NMC_RESIDENT_IDLE_US");
