@@ -139,12 +139,14 @@ int nmc_prefill_stats(nmc_ctx* ctx, int64_t* issued, int64_t* used);
  * (Sampler._loop :872-891 driven in chunks, e.g. samplePosterior's progress
  * steps): a call that continues where the previous one ended is handed to the
  * running launch (a command word in pinned host memory) instead of a new launch;
- * the rows and chain state stay in LDS.  Each call is closed as a launch is --
- * after nmc_synchronize its sample rows, hyper-parameters and state are in HBM,
- * bit for bit those of separate launches.  Any other entry point parks the
- * launch first; it parks itself after NMC_RESIDENT_IDLE_US (20 ms) without a
- * call.  No effect where the context's kernel has no resident form (enabled 0
- * in nmc_resident_stats).  No reference counterpart: host plumbing.          */
+ * the rows and chain state stay in LDS.  Each call completes its results as a
+ * launch does -- after nmc_synchronize its sample / trace rows and hyper-
+ * parameters are in HBM, bit for bit those of separate launches; the chain
+ * state reaches HBM when the launch parks.  Any other entry point parks the
+ * launch first (so every read sees the state of separate launches); it parks
+ * itself after NMC_RESIDENT_IDLE_US (20 ms) without a call.  No effect where
+ * the context's kernel has no resident form (enabled 0 in nmc_resident_stats).
+ * No reference counterpart: host plumbing.                                   */
 int nmc_set_resident(nmc_ctx* ctx, int enable);
 /* enabled: resident launches possible and on; active: one is running now;
  * launches / calls: resident launches made / calls continued inside one;

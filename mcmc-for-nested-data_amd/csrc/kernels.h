@@ -2229,13 +2229,13 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   // ---- resident launch: the end of a call (t == ie), every wave (uniform) ----
   // The call's results are completed as a launch completes them -- the last publication
   // counted, the pending step's state update and sample / trace stores, the call's last Gibbs
-  // tasks (register mode: by every workgroup's Gibbs wave for its own hyper state, as the
-  // in-loop tasks are; group 0's writes them through and records them) -- and every wave's
-  // stores drained; the workgroup counts itself done (the last one of the grid tells the
-  // host: pinned memory) and takes the next command: workgroup 0 polls the host's command
-  // word and relays it, the others poll the relay of their XCD.  On a new end: the first
-  // step's variates; the Gibbs pipeline restarts as at a launch's start (gfirst), so the next
-  // call runs exactly as a new launch of [t, end) would.  The chain state (values, scales,
+  // tasks (register mode: the workgroups of groups 0 .. lag-1, written through and recorded)
+  // -- and every wave's stores drained; the workgroup counts itself done (the last one of the
+  // grid tells the host: pinned memory) and takes the next command: workgroup 0 polls the
+  // host's command word and relays it, the others poll the relay of their XCD.  On a new
+  // end: the first step's variates and the hyper-parameters reloaded as a launch's prologue
+  // loads them; the Gibbs pipeline restarts as at a launch's start (gfirst), so the next call
+  // runs exactly as a new launch of [t, end) would.  The chain state (values, scales,
   // counters, priors, group LLs) stays in LDS and is written to HBM when the launch parks.
   // false: the launch ends (park, or a timeout in d.tmo).
   unsigned rseq = d.rseq, rcall = 0;   // (rcall: calls of this launch done)
@@ -2261,16 +2261,15 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
         if (pend_p >= 0) apply_pending();
         store_pending();
       }
-      // the call's last Gibbs tasks, by every workgroup's Gibbs wave for its own hyper state
-      // as the in-loop tasks are (group 0's writes and records them)
-      if constexpr (hr && decltype(gibbs)::value) {
-        const int ge = ie * P;
-        for (int k = ge - lag > gfirst ? ge - lag : gfirst; k < ge; ++k) {
-          const int kq = k % P, kt = k / P;
-          if (!nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1))) break;
-          // keep the payload loads below the poll (no instruction: wavefront scope)
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          nmc_hyper_update_reg(d, cb, kt, kq, cc, lds, L.hyp, g0w);
+      // the call's last Gibbs tasks, as a launch closes them: task ge-lag+j by the workgroup
+      // of group j, written through and recorded (every workgroup reloads them below)
+      if constexpr (hr) {
+        const int ck = close_of(ie);
+        if (ck >= 0) {
+          const bool pub = nmc_wait_published(d, cb, ck % P,
+                                              (unsigned)G * (unsigned)(ck / P - i0 + 1), lds, L);
+          if constexpr (decltype(gibbs)::value)
+            if (pub) nmc_hyper_update_reg(d, cb, ck / P, ck % P, cc, lds, L.hyp, true);
         }
       }
       nmc_drain_vm();
@@ -2373,6 +2372,23 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
       __syncthreads();
       const double e = lds[L.flag * 64 + 2];
       if (e < 0.0) return false;
+      if constexpr (hr) {   // the hyper-parameters after iteration t - 1, as a launch's
+                            // prologue loads them (parameter p by wave p % W; sc1: the closing
+                            // workgroups wrote them through before the call was reported done)
+        for (int p = w; p < P; p += W) {
+          const size_t ho = nmc_hslot(d, t - 1) + (size_t)p * C + cc;
+          const double s2 = nmc_ldv<NMC_SRC_SC1>(d.s2 + ho);
+          const double m = nmc_ldv<NMC_SRC_SC1>(d.mu + ho);
+          const double sd = nmc_ldv<NMC_SRC_SC1>(d.hsd + ho);
+          const double lsd = nmc_ldv<NMC_SRC_SC1>(d.hlsd + ho);
+          hy[(NMC_HY_MU * P + p) * 64] = m;
+          hy[(NMC_HY_SD * P + p) * 64] = sd;
+          hy[(NMC_HY_LSD * P + p) * 64] = lsd;
+          hy[(NMC_HY_S2 * P + p) * 64] = s2;
+          hy[(NMC_HY_SDM * P + p) * 64] = sqrt(s2 / G);
+          hy[(NMC_HY_ISD * P + p) * 64] = 1.0 / sd;
+        }
+      }
       nmc_drain_vm();   // (the control wave's variate DMA has landed)
       __syncthreads();
       ie = (int)e;
@@ -2384,28 +2400,24 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   if constexpr (hr) if (gw) {
     const int gs0 = i0 * P;
     (void)gs0;   // (the control-path stamps build)
-    // (calls: the steps of [t, ie), then -- resident launch -- the gate to the next call,
-    //  outside the step loop: its Gibbs updates then share no live range with the loop's)
-    for (int t = i0;;) {
-      for (; t < ie && ok; ++t) {
-        for (int p = 0; p < P; ++p) {
-          dP = nmc_kdev();
-          const int gs = t * P + p;
-          const bool due = gs - lag >= gfirst;
-          gibbs_step(t, p);
+    for (int t = i0; ok; ++t) {
+      if (t == ie && !res_gate(t, nmc_bool_c<true>{})) break;
+      for (int p = 0; p < P; ++p) {
+        dP = nmc_kdev();
+        const int gs = t * P + p;
+        const bool due = gs - lag >= gfirst;
+        gibbs_step(t, p);
 #if NMC_GIBBS_TILES   // (A/B build option: the Gibbs wave takes likelihood tiles after its task)
-          lik_tiles(t, p, gs & 1, [] {});
+        lik_tiles(t, p, gs & 1, [] {});
 #endif
-          NMC_CS(gs - gs0, w);
-          nmc_run_barrier();   // A
-          if (due) {
-            ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
-            if (!ok) break;
-          }
-          nmc_run_barrier();   // B
+        NMC_CS(gs - gs0, w);
+        nmc_run_barrier();   // A
+        if (due) {
+          ok = lds[L.flag * 64 + 1] == 2.0 * ((double)gs + 1);
+          if (!ok) break;
         }
+        nmc_run_barrier();   // B
       }
-      if (!ok || !res_gate(t, nmc_bool_c<true>{})) break;
     }
     // closing: tasks ge-lag .. ge-1, task ge-lag+j by the workgroup of group j (member 0),
     // which writes and records it -- in parallel, not one after the other; the same

@@ -489,8 +489,9 @@ static int res_continue(nmc_ctx* x, int i0, int i1) {
   x->d.xbase += (unsigned)((i1 - i0) * x->P);
   x->cur_slot = (i1 - 1) & 1;
   // the next call's variates beside this one (the same length, while the schedule and the
-  // buffer last)
-  if (x->prefill_on) {
+  // buffer last; NMC_RES_PREFILL=0, diagnostics: none -- the next call then launches anew)
+  static const bool res_prefill_on = !(getenv("NMC_RES_PREFILL") && !atoi(getenv("NMC_RES_PREFILL")));
+  if (x->prefill_on && res_prefill_on) {
     const int n1 = std::min({i1 + (i1 - i0), x->n_iter, r.vbase + x->d.vcap});
     if (n1 > i1)
       if (int rc = res_prefill(x, i1, n1)) return rc;
@@ -1305,6 +1306,11 @@ int nmc_set_resident(nmc_ctx* x, int enable) {
     r.fill_minb = left >= 144 ? 1 : left >= 128 ? 4 : left >= 96 ? 5 : left >= 80 ? 6
                 : left >= 64 ? 8 : 0;
     if (!r.fill_minb) return 0;
+    // (diagnostics, A/B: a smaller fill instance than the one that fits)
+    if (const char* e = getenv("NMC_RES_FILL_MINB")) {
+      const int v = atoi(e);
+      if ((v == 4 || v == 5 || v == 6 || v == 8) && v > r.fill_minb) r.fill_minb = v;
+    }
   }
   if (!r.host) {
     const size_t bytes = 512;
