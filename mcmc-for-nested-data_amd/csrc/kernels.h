@@ -2008,6 +2008,14 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
     // both tile counters start at the static entries: waves 2 .. W-1 begin on entries
     // 0 .. W-3 by rank, without a take (every wave from 2 on runs lik_tiles in every mode)
     if (lane < 2) tcnt[lane] = (unsigned)(nstatic && W > 2 ? W - 2 : 0);
+    if (RES && b == 0 && lane == 0) {   // the launch's own call taken now (its GPU span)
+      const unsigned long long clk = __builtin_amdgcn_s_memrealtime();
+      __hip_atomic_store(d.rack + 2, (unsigned)clk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(d.rack + 3, (unsigned)(clk >> 32), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      nmc_drain_vm();
+      __hip_atomic_store(d.rack, d.rseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   __syncthreads();
   NMC_RUN_SL(1);

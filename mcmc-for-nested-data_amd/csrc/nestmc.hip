@@ -1238,9 +1238,9 @@ int nmc_eval_obs_ll(nmc_ctx* x, double* out) {
 }
 
 // With a resident launch on the stream an event would complete only when the launch ends:
-// the slot marks the latest call issued instead, and the elapsed time between two marks is
-// the sum of the GPU spans (s_memrealtime: workgroup 0 taking the call -> the last workgroup
-// done) of the calls issued between them.
+// the slot marks the latest call issued instead, and the elapsed time up to such a mark is
+// the sum of the GPU spans (s_memrealtime: workgroup 0 taking the call, or starting the
+// launch for its first call -> the last workgroup done) of the calls issued since slot a.
 int nmc_event_record(nmc_ctx* x, int slot) {
   if (slot < 0 || slot >= 16) return fail(-1, "event slot 0..15");
   hipSetDevice(x->device);
@@ -1254,9 +1254,7 @@ int nmc_event_elapsed(nmc_ctx* x, int a, int b, float* ms) {
   if (a < 0 || a >= 16 || b < 0 || b >= 16) return fail(-1, "event slot 0..15");
   hipSetDevice(x->device);
   auto& r = x->res;
-  if (r.ev_res[a] || r.ev_res[b]) {
-    if (!(r.ev_res[a] && r.ev_res[b]))
-      return fail(-1, "event slots on both sides of a resident launch's start or park");
+  if (r.ev_res[b]) {   // (a: a marker, or an event recorded before the launch started)
     if ((int)(r.ev_seq[b] - r.done) > 0)
       if (int rc = res_wait_done(x)) return rc;
     double sum = 0;
@@ -1264,13 +1262,14 @@ int nmc_event_elapsed(nmc_ctx* x, int a, int b, float* ms) {
       auto it = std::find_if(r.spans.begin(), r.spans.end(),
                              [&](const std::pair<unsigned, double>& e) { return e.first == q; });
       if (it == r.spans.end() || it->second < 0)
-        return fail(-1, "no GPU span for a call between the event slots (the launch's first "
-                        "call, or a parked one)");
+        return fail(-1, "no GPU span for a call between the event slots (a call of a launch "
+                        "that has parked since)");
       sum += it->second;
     }
     *ms = (float)sum;
     return 0;
   }
+  if (r.ev_res[a]) return fail(-1, "event slot a marks a resident call, b does not");
   HIPCHK(hipEventSynchronize(x->ev[b]));
   HIPCHK(hipEventElapsedTime(ms, x->ev[a], x->ev[b]));
   return 0;
