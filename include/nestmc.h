@@ -154,7 +154,8 @@ int nmc_set_resident(nmc_ctx* ctx, int enable);
  * 2 kernel timing, 3 longer than a chunk, 4 past the launch's variate buffer,
  * 5 variates not prefilled there, 6 counters would wrap, 7 the launch had
  * parked itself after its idle limit, 8 its prefill did not finish beside
- * the launch within 2 ms).                                                    */
+ * the launch within 2 ms -- kernels serialized, e.g. by a profiler's counter
+ * pass: the resident form is then turned off for the context).               */
 int nmc_resident_stats(nmc_ctx* ctx, int* enabled, int* active, int64_t* launches,
                        int64_t* calls, int* last_refusal);
 

@@ -451,7 +451,10 @@ static int res_continue(nmc_ctx* x, int i0, int i1) {
     const auto tq = std::chrono::steady_clock::now();
     while (hipEventQuery(x->pf_ev) != hipSuccess) {
       if (std::chrono::steady_clock::now() - tq > std::chrono::milliseconds(2)) {
+        // (kernels serialized -- a profiler's counter pass does it -- or no room beside the
+        //  launch: later calls launch as they would without nmc_set_resident)
         r.why = 8;
+        r.on = false;
         RES_PARK(x);
         return 0;
       }
