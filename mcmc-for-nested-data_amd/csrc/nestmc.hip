@@ -1147,11 +1147,21 @@ int nmc_synchronize(nmc_ctx* x) {
   // the step stream, then the prefill stream (a prefill is part of the work a call enqueued)
   for (hipStream_t s : {x->stream, x->pstream}) {
     if (s == x->stream && x->res.active) continue;
+    const auto ts = std::chrono::steady_clock::now();
     for (;;) {
       const hipError_t e = poll_us > 0 ? hipStreamQuery(s) : hipErrorNotReady;
       ++nq;
       if (e == hipSuccess) break;
       if (e != hipErrorNotReady) return fail(-2, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+      // a prefill that has not finished 2 ms after the resident call did: it cannot run beside
+      // the launch (kernels serialized, e.g. a profiler's counter pass) -- park the launch so
+      // that it runs, and launch from now on (nmc_resident_stats reason 8)
+      if (x->res.active &&
+          std::chrono::steady_clock::now() - ts > std::chrono::milliseconds(2)) {
+        x->res.why = 8;
+        x->res.on = false;
+        RES_PARK(x);
+      }
       const auto dt = std::chrono::steady_clock::now() - t0;
       if (dt >= std::chrono::microseconds(poll_us)) {
         HIPCHK(hipStreamSynchronize(s));
