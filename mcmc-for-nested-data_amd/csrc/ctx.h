@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <utility>
 #include <vector>
@@ -100,6 +101,7 @@ struct nmc_ctx {
     long long launches = 0, calls = 0;    // resident launches / calls continued in one
     int why = 0;                          // why the latest call was not continued (0: it was)
     int fill_minb = 1;                    // nmc_k_fill instance that fits beside the launch
+    std::chrono::steady_clock::time_point t_post;   // (NMC_TRACE_CALLS: the latest post)
     std::vector<std::pair<unsigned, double>> spans;   // (seq, GPU ms) of continued calls
     bool ev_res[16] = {};                 // event slot recorded as a resident marker
     unsigned ev_seq[16] = {};

@@ -380,9 +380,12 @@ static int res_wait_done(nmc_ctx* x) {
     const unsigned long long e = clk(0), le = clk(1), st = clk(2);
     r.spans.emplace_back(r.seq, e >= a ? (double)(e - a) / 1e5 : -1.0);
     if (g_trace_calls)   // (the critical path: the last workgroup to start, to end its loop)
-      fprintf(stderr, "[nmc trace] resident call %u: relay %.2f loop %.2f close %.2f us\n",
+      fprintf(stderr, "[nmc trace] resident call %u: relay %.2f loop %.2f close %.2f us; host "
+              "post -> done seen %.2f us\n",
               r.seq, ((double)st - (double)a) / 100.0, ((double)le - (double)st) / 100.0,
-              ((double)e - (double)le) / 100.0);
+              ((double)e - (double)le) / 100.0,
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() -
+                                                        r.t_post).count());
     if (r.spans.size() > 64) r.spans.erase(r.spans.begin(), r.spans.begin() + 32);
   }
   r.done = r.seq;
@@ -443,7 +446,9 @@ static int res_continue(nmc_ctx* x, int i0, int i1) {
     RES_PARK(x);
     return 0;
   }
+  const auto t_in = std::chrono::steady_clock::now();
   if (int rc = res_wait_done(x)) return rc;
+  const auto t_wd = std::chrono::steady_clock::now();
   // the call's variates have landed (the prefill runs beside the launch, which it fits:
   // nmc_set_resident); a prefill not done within 2 ms parks the launch rather than wait
   // for its idle limit -- whatever held the fill back, it cannot start beside the launch
@@ -462,11 +467,24 @@ static int res_continue(nmc_ctx* x, int i0, int i1) {
     }
   }
   const unsigned seq = r.seq + 1;
+  const auto t_post = std::chrono::steady_clock::now();
   *r.cmd = ((unsigned long long)(unsigned)i1 << 32) | seq;
+  std::atomic_thread_fence(std::memory_order_seq_cst);   // (out of the store buffer now)
   r.seq = seq;
+  r.t_post = t_post;
   // taken, or workgroup 0 parked (idle) before it saw the command
   for (unsigned long spins = 0;; ++spins) {
-    if (r.ack[0] == seq) break;
+    if (r.ack[0] == seq) {
+      if (g_trace_calls) {
+        auto us = [&](std::chrono::steady_clock::time_point t) {
+          return std::chrono::duration<double, std::micro>(t - t_in).count();
+        };
+        fprintf(stderr, "[nmc trace] resident call %u: host done-wait %.2f prefill-query %.2f "
+                "ack seen %.2f us\n", seq, us(t_wd), us(t_post),
+                us(std::chrono::steady_clock::now()));
+      }
+      break;
+    }
     if (r.ack[1] == (0x80000000u | (seq - 1))) {
       r.why = 7;
       r.done = seq;
