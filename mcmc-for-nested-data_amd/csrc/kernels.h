@@ -327,7 +327,12 @@ __device__ __forceinline__ size_t nmc_hslot(const Dev& d, int t) {
 }
 
 __device__ __forceinline__ int nmc_record_row(const Dev& d, int iter) {
-  if (iter < d.burn || (iter % d.thin) != 0) return -1;
+  if (iter < d.burn) return -1;
+  if (d.thin == 1) {   // (every post-burn iteration: no integer divisions on the step's path)
+    const int row = iter - d.burn;
+    return row < d.n_rows ? row : -1;
+  }
+  if ((iter % d.thin) != 0) return -1;
   const int first = ((d.burn + d.thin - 1) / d.thin) * d.thin;
   const int row = (iter - first) / d.thin;
   return row < d.n_rows ? row : -1;

@@ -5,7 +5,11 @@ libnestmc prints the host time of nmc_run's and nmc_synchronize's phases; this s
 prints per call the Python-side wall time, the event time on the stream and the step
 kernel's own time (kernel-timing events).
 
-    python tools/calltrace.py [K] [R]
+    python tools/calltrace.py [K] [R] [resident] [norec]
+
+(resident=1: the calls share one resident step launch, nmc_set_resident; no kernel-timing
+calls then, which would park it; norec=1: the calls' iterations are burn-in, no sample rows
+written -- the recording's cost; norec=2: post-burn, thinned to one row)
 """
 import os
 import sys
@@ -21,18 +25,25 @@ def main():
     import bench
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     R = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+    res = len(sys.argv) > 3 and sys.argv[3] == "1"
     wl = dict(bench.WORKLOADS["cfg3"])
     eng, _, _ = bench.make_engine(wl, 0, 1, 0)
     W = 5
     n_iter = W + (R + 1) * K
-    eng.set_schedule(n_iter, W, 1)
+    norec = sys.argv[4] if len(sys.argv) > 4 else "0"
+    # (2: post-burn but thinned to one row -- recording off, tuning off too)
+    eng.set_schedule(n_iter, n_iter - 1 if norec == "1" else W,
+                     n_iter - W if norec == "2" else 1)
     eng.set_launch_iters(0)
+    if res:
+        eng.set_resident(True)
     eng.run(0, W)
     eng.prefill(W, W + K)
     eng.synchronize()
     for r in range(R):
         i0 = W + r * K
-        eng.set_kernel_timing(r % 2 == 1)
+        kt_on = r % 2 == 1 and not res
+        eng.set_kernel_timing(kt_on)
         eng.event_record(0)
         t0 = time.perf_counter()
         eng.run(i0, i0 + K)
@@ -41,7 +52,7 @@ def main():
         eng.synchronize()
         wall = time.perf_counter() - t0
         ev = eng.event_elapsed_ms(0, 1)
-        kt = eng.kernel_timing() if r % 2 == 1 else None
+        kt = eng.kernel_timing() if kt_on else None
         sys.stderr.flush()
         print("call %d: wall_us %.1f event_us %.1f enqueue_us %.1f kernel_us %s"
               % (r, wall * 1e6, ev * 1e3, t_enq * 1e6,
