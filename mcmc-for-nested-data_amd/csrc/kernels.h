@@ -2187,7 +2187,8 @@ nmc_k_run(Dev d_arg, Fam fam, const double* __restrict__ obs, int i0, int i1, in
   auto gibbs_step = [&](int t, int p) {
     const int gs = t * P + p;
     if (gs - lag < gfirst) return;
-    const int k = gs - lag, kq = k % P, kt = k / P;
+    // task gs - lag as (kt, kq) without dividing by P (lag <= P)
+    const int kq = p >= lag ? p - lag : p - lag + P, kt = p >= lag ? t : t - 1;
     NMC_CS(gs - i0 * P, 24);
     const bool r = nmc_poll_published(d, cb, kq, (unsigned)G * (unsigned)(kt - i0 + 1));
     NMC_CS(gs - i0 * P, 25);
